@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Benchmark: patterns/sec (count + locate) on BASELINE.json's headline config.
+
+Workload (BASELINE.json configs[1], "C2"): 1 Gbp uniform ACGT text, symbols
+ACGTN (N = wildcard, sigma 5), layout u32 / Block3<u64> / EncodingTable,
+SA sampling 2, k-mer table k = 3; 100,000 x 20 bp patterns cut from the text at
+uniform random starts (bench/src/generate.rs:105-113, cold ratio 1.0), per GPU.
+
+One step = one fmx_locate_batch_async call over the batch: k-mer seed + LF loop
+(k_count), exclusive scan of the counts, sampled-SA walk (k_locate) — every
+count and every location of every pattern, written to HBM.  Inputs (text,
+blob, patterns) are resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU (torchrun); each rank builds its own replica of
+the blob on its GPU (deterministic), runs its own pattern batch (weak scaling,
+no collective in the timed region) and the counts are all-gathered over RCCL
+afterwards (result concatenation, timed separately).
+
+Also reported: the dominant kernel's roofline (HIP events on the engine's
+stream), a CPU baseline (the oracle restatement on this host, rank 0), and a
+bit-exact check of the GPU results against it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "patterns/sec (count+locate), 1 Gbp text / 20 bp patterns, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--text-len", type=int, default=1_000_000_000)
+    ap.add_argument("--patterns", type=int, default=100_000, help="patterns per GPU per step")
+    ap.add_argument("--pattern-len", type=int, default=20)
+    ap.add_argument("--occ", default="interleaved", choices=["interleaved", "blob"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--traffic-csv", default=os.path.join(ROOT, "profiles", "r01_pmc_fetch_size.json"))
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__ as g
+    pkg = g.load_package()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    n, B, m = args.text_len, args.patterns, args.pattern_len
+    # ---- synthetic text (same on every rank: the blob is replicated) -------
+    t0 = time.time()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed)
+    acgt = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    d_text = acgt[torch.randint(0, 4, (n,), device=dev, dtype=torch.int64, generator=gen)]
+    table = pkg.text_encoders.EncodingTable.from_symbols([b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"])
+    block = pkg.blocks.Block3(pkg.Vector.U64)
+    builder = (pkg.FmIndexBuilder(n, table.symbol_count(), table, pkg.u32, block)
+               .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+               .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    blob_len = builder.blob_size()
+    d_blob = torch.empty(blob_len, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t1 = time.time()
+    builder.build_device(d_text.data_ptr(), d_blob.data_ptr(), blob_len, device=local)
+    torch.cuda.synchronize()
+    build_s = time.time() - t1
+    log(f"[rank {rank}] text {n:,} B generated in {t1 - t0:.2f}s, blob {blob_len:,} B built on GPU in {build_s:.2f}s")
+    ix = pkg.FmIndex.load_device(d_blob.data_ptr(), blob_len, pkg.u32, block, pkg.text_encoders.EncodingTable,
+                                 device=local, occ=args.occ)
+    info = ix.info()
+
+    # ---- patterns: substrings at uniform starts (per-rank seed) ------------
+    pg = torch.Generator(device=dev)
+    pg.manual_seed(args.seed * 1000 + 7 + rank)
+    starts = torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg)
+    d_pat = d_text[(starts[:, None] + torch.arange(m, device=dev)[None, :]).reshape(-1)].contiguous()
+    d_off = (torch.arange(B + 1, device=dev, dtype=torch.int64) * m).contiguous()
+    cap = 4 * B + 4096
+    d_loff = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+    d_locs = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_need = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = ix.locate_workspace_size(B)
+    d_ws = torch.empty(ws, dtype=torch.uint8, device=dev)
+
+    def step():
+        ix.locate_batch_async(d_pat.data_ptr(), d_off.data_ptr(), B, d_loff.data_ptr(), d_locs.data_ptr(), cap,
+                              d_need.data_ptr(), d_ws.data_ptr(), ws)
+
+    for _ in range(args.warmup):
+        step()
+    ix.sync()
+    need = int(d_need.item())
+    if need > cap:
+        raise SystemExit(f"location buffer too small: {need} > {cap}")
+
+    # ---- timed region ------------------------------------------------------
+    ix.timing_read()          # drain warmup events
+    ix.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+    ix.timing_enable(False)
+    ix.sync()
+    timing = ix.timing_read()
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # ---- result concatenation across ranks (RCCL all-gather, untimed) ------
+    gather_ms = None
+    if world > 1:
+        cnt = (d_loff[1:] - d_loff[:-1]).to(torch.int32)
+        outs = [torch.empty_like(cnt) for _ in range(world)]
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        dist.all_gather(outs, cnt)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    # ---- roofline of the dominant kernel ------------------------------------
+    P, BLK = 4, 24                      # u32 positions, Block3<u64> = 24 B
+    k = info["kmer_size"]
+    offs_h = d_loff.cpu().numpy().view(np.uint64)
+    total_occ = int(offs_h[-1])
+    # every pattern is cut from the text, so its interval never empties and the
+    # LF loop runs exactly m - k steps (with_slice.rs:27-31)
+    L = m - k
+    count_bytes_per_pattern = m + 8 + 2 * P + L * 2 * (P + BLK) + 8 + P   # pattern, offset, seed, LF, cnt64+lo
+    locate_bytes_per_occ = 1.0 * (P + BLK) + P + P                          # E[walk]=sr-1 steps, SA, output
+    kern = {}
+    for name, t in timing.items():
+        kern[name] = t["total_ms"] / max(t["launches"], 1)
+    dominant = max(kern, key=kern.get) if kern else "count"
+    if dominant == "locate":
+        alg_bytes = locate_bytes_per_occ * total_occ + (P + 16) * B
+    else:
+        alg_bytes = count_bytes_per_pattern * B
+    achieved = alg_bytes / (kern.get(dominant, float("nan")) * 1e-3) / 1e9
+    traffic = None
+    traffic_src = None
+    if os.path.exists(args.traffic_csv):
+        try:
+            pm = json.load(open(args.traffic_csv))
+            if pm.get("config") == f"{n}:{B}:{m}:{args.occ}" and dominant in pm.get("per_launch_bytes", {}):
+                traffic = pm["per_launch_bytes"][dominant]
+                traffic_src = os.path.relpath(args.traffic_csv, ROOT)
+        except Exception:
+            pass
+
+    value = world * B * args.steps / elapsed
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "patterns/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: seeded uniform ACGT text; patterns cut from it at uniform random starts",
+        "config": {
+            "workload": f"C2: {n:,} bp ACGT text (ACGTN, N wildcard), {B:,} x {m} bp patterns per GPU, "
+                        f"u32/Block3<u64>/EncodingTable, SA sampling 2, k-mer LUT 3",
+            "text_len": n, "patterns_per_gpu": B, "pattern_len": m, "occ_layout": args.occ,
+            "parallelism": f"dp{world} (patterns sharded, blob replicated)",
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kern.get(dominant),
+        },
+        "kernels_ms_per_launch": kern,
+        "occurrences_per_step": total_occ,
+        "build_s": build_s,
+        "gather_ms": gather_ms,
+    }
+
+    # ---- CPU baseline + bit-exact check (rank 0, N=1 only) -------------------
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        host_blob = O.aligned_zeros(blob_len, 16)
+        host_blob[:] = d_blob.cpu().numpy()
+        L_ = O.layout(4, 3, 64, 0)
+        orc = O.OracleIndex(host_blob, L_)
+        pats_h = d_pat.cpu().numpy()
+        offs_in = np.arange(B + 1, dtype=np.uint64) * m
+        # 1 thread, whole passes over the batch until the budget is spent
+        done, tc = 0, time.perf_counter()
+        ooff = olocs = None
+        while True:
+            ooff, olocs = orc.locate_batch(pats_h, offs_in, threads=1, cap=cap)
+            done += B
+            if time.perf_counter() - tc >= args.cpu_seconds:
+                break
+        cpu1 = done / (time.perf_counter() - tc)
+        tc = time.perf_counter()
+        orc.locate_batch(pats_h, offs_in, threads=args.cpu_threads, cap=cap)
+        cpun = B / (time.perf_counter() - tc)
+        glocs = d_locs[:total_occ].cpu().numpy().view(np.uint32)
+        exact = bool(np.array_equal(ooff, offs_h) and np.array_equal(olocs, glocs))
+        cores = os.cpu_count()
+        try:
+            model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
+        except Exception:
+            model = "unknown"
+        result["cpu_baseline"] = {
+            "value": cpu1, "unit": "patterns/s", "cores": 1, "kind": "port",
+            "sample": f"{done:,} patterns = {done // B} passes over the same {B:,}-pattern batch, "
+                      f"oracle/fmx_oracle.c (C restatement of the reference query path), blob in RAM",
+            f"value_{args.cpu_threads}_threads": cpun, "cpu_model": model, "host_cpus_visible": cores,
+        }
+        result["parity"] = {"bit_exact_vs_cpu": exact, "patterns": B, "occurrences": total_occ}
+        result["speedup_vs_cpu_1thread"] = value / cpu1
+        result[f"speedup_vs_cpu_{args.cpu_threads}_threads"] = value / cpun
+        if not exact:
+            log("PARITY FAILURE: GPU results differ from the CPU oracle")
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ix.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

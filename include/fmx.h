@@ -1,0 +1,186 @@
+/*
+ * fmx.h — C ABI of the MI355X-native batched FM-index count/locate engine.
+ *
+ * This is the drop-in boundary for baku4/sview-fmindex's query hot path.  The
+ * reference has no FFI of its own: its surface is the Rust generic API
+ * `FmIndex<'a, P: Position, B: Block, E: TextEncoder>` (sview-fmindex/src/lib.rs:14-28)
+ * over the blob byte layout written by `FmIndexBuilder::build`
+ * (src/builder/mod.rs:187-264).  Each entry point below names the reference
+ * item it replaces; INTEGRATION.md shows the Rust `extern "C"` binding a
+ * maintainer would add to restore `FmIndex::count/locate` on top of it.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  "Host" buffers are ordinary CPU memory;
+ *    "device" buffers are HIP device pointers on the index's device.
+ *  - P-wide outputs (counts, locations) are uint32_t when layout.pos_bytes == 4
+ *    and uint64_t when 8, exactly the reference's `P` (src/text_length.rs:10-129).
+ *  - Locations of one pattern are emitted in suffix-array-row order, the order
+ *    `FmIndex::locate` returns them in (src/locate/mod.rs:14-37).
+ *  - No entry point aborts: every failure the reference reports as an error or
+ *    a panic is returned as an fmx_status.
+ */
+#ifndef FMX_H
+#define FMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMX_ABI_VERSION 1u
+
+typedef enum fmx_status {
+    FMX_OK = 0,
+    FMX_E_FORMAT = 1,        /* LoadError::InvalidFormat (src/load_from_blob.rs:16-19, 31-33)          */
+    FMX_E_SIZE = 2,          /* LoadError::MismatchedBlobSize(expected, actual) (load_from_blob.rs:20-23, 46-58) */
+    FMX_E_ALIGN = 3,         /* misaligned blob: reference panics (bwm/mod.rs:172-181); BuildError::NotAlignedBlob */
+    FMX_E_LAYOUT = 4,        /* layout tag inconsistent with the blob's headers (P/B/E are not stored in the blob) */
+    FMX_E_EMPTY_PATTERN = 5, /* empty pattern: reference panics (components/count_array.rs:211)            */
+    FMX_E_SYMBOL = 6,        /* PassThrough byte >= symbol_count; BuildError::SymbolCountOver (builder/mod.rs:71-73) */
+    FMX_E_CAPACITY = 7,      /* locate output buffer smaller than the number of occurrences ("needed")   */
+    FMX_E_DEVICE = 8,        /* HIP runtime error, or no GPU                                               */
+    FMX_E_ARG = 9,           /* null pointer or invalid argument                                           */
+    FMX_E_CONFIG = 10        /* BuildError::{InvalidConfig, UnmatchedTextLength, InvalidBlobSize}          */
+} fmx_status;
+
+/* The reference's type parameters, which the blob does not record
+ * (only sizes are checked, src/load_from_blob.rs:40-58). */
+typedef struct fmx_layout {
+    uint32_t pos_bytes; /* P: 4 = u32, 8 = u64                      (src/text_length.rs:10-129)   */
+    uint32_t planes;    /* B = BlockN<V>: N in 2..6                  (components/bwm/blocks/mod.rs)  */
+    uint32_t vec_bits;  /* V: 32, 64 or 128 = BLOCK_LEN              (components/bwm/blocks/vector.rs:11-79) */
+    uint32_t encoder;   /* E: FMX_ENC_TABLE or FMX_ENC_PASS          (components/text_encoder/)      */
+} fmx_layout;
+
+#define FMX_ENC_TABLE 0u /* EncodingTable([u8; 256])  text_encoders/encoding_table.rs:7-11 */
+#define FMX_ENC_PASS 1u  /* PassThrough               text_encoders/pass_through.rs:6-12   */
+
+/* Query flags */
+#define FMX_PATTERN_REVERSED 1u /* patterns are given last byte first: the *_rev_iter forms
+                                   (src/locate/with_rev_iter.rs:5-38)                          */
+
+/* Device occ representation chosen at load (results are identical). */
+#define FMX_OCC_BLOB 0u        /* kernels read the blob's rank_checkpoints / blocks as laid out  */
+#define FMX_OCC_INTERLEAVED 1u /* checkpoints + bit planes re-laid out into one HBM line per block */
+
+typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
+
+typedef struct fmx_index_info {
+    uint64_t text_len;       /* C[symbol_count]                                   */
+    uint64_t sentinel_index; /* BwmView.sentinel_index                            */
+    uint64_t blob_len;
+    uint64_t device_bytes;   /* HBM held by the index (blob + any re-layout)      */
+    uint32_t symbol_count;
+    uint32_t kmer_size;      /* lookup_table_kmer_size                            */
+    uint32_t sampling_ratio;
+    uint32_t block_len;      /* BLOCK_LEN = vec_bits                              */
+    uint32_t occ_mode;       /* FMX_OCC_*                                         */
+    int32_t device;
+} fmx_index_info;
+
+typedef struct fmx_kernel_timing {
+    char name[32];
+    uint64_t launches;
+    double total_ms;         /* summed hipEvent durations on the launch stream    */
+    uint64_t units;          /* patterns (count) or occurrences (locate) processed */
+} fmx_kernel_timing;
+
+/* ---------------------------------------------------------------- version */
+uint32_t fmx_abi_version(void);
+const char *fmx_status_str(fmx_status s);
+int fmx_device_count(void);
+
+/* ------------------------------------------------------------------- load */
+
+/* FmIndex::load (src/load_from_blob.rs:28-85).  Validates the blob exactly as
+ * the reference does (magic + version, header sizes, exact body size) plus the
+ * consistency checks the reference leaves to the type system, then copies the
+ * blob to HBM of `device` once.  The host blob is borrowed for fmx_blob() only.
+ * On FMX_E_SIZE, *expected_total / *actual_total receive the two sizes.
+ * occ_mode: FMX_OCC_BLOB or FMX_OCC_INTERLEAVED. */
+fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, int device,
+                    uint32_t occ_mode, fmx_index **out, uint64_t *expected_total,
+                    uint64_t *actual_total);
+
+/* Same, for a blob already resident in HBM of `device` (e.g. written by
+ * fmx_build_device).  The device blob is borrowed and must outlive the index. */
+fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout layout, int device,
+                           uint32_t occ_mode, fmx_index **out, uint64_t *expected_total,
+                           uint64_t *actual_total);
+
+void fmx_free(fmx_index *ix);
+
+/* FmIndex::blob (src/reference_to_source_blob.rs:9-11).  NULL for device loads. */
+const uint8_t *fmx_blob(const fmx_index *ix, uint64_t *len);
+
+fmx_status fmx_info(const fmx_index *ix, fmx_index_info *out);
+
+/* ---------------------------------------------- queries on host buffers
+ * Synchronous.  Patterns are ragged: pattern i is bytes[offsets[i] .. offsets[i+1]). */
+
+/* FmIndex::count / count_rev_iter (locate/with_slice.rs:5-8, with_rev_iter.rs:5-9), batched. */
+fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets,
+                           uint64_t n_patterns, uint32_t flags, void *out_counts);
+
+/* FmIndex::locate / locate_rev_iter (with_slice.rs:10-13, with_rev_iter.rs:10-14),
+ * batched: the locations of pattern i are out_locs[out_loc_offsets[i] ..
+ * out_loc_offsets[i+1]) in suffix-array-row order.  *needed receives the total;
+ * if it exceeds cap, nothing past cap is written and FMX_E_CAPACITY is returned. */
+fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets,
+                            uint64_t n_patterns, uint32_t flags, uint64_t *out_loc_offsets,
+                            void *out_locs, uint64_t cap, uint64_t *needed);
+
+/* ---------------------------------------------- queries on device buffers
+ * Asynchronous on `stream` (a hipStream_t; NULL = the index's own stream).
+ * Inputs and outputs live in HBM of the index's device.  Errors detected on
+ * the device (empty pattern, PassThrough symbol) are latched in a status word
+ * read by fmx_sync(). */
+
+fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
+                                 uint64_t n_patterns, uint32_t flags, void *d_counts, void *stream);
+
+/* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns. */
+fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
+
+/* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)
+ * receives P-wide counts; d_needed (device uint64) receives the total. */
+fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
+                                  uint64_t n_patterns, uint32_t flags, void *d_counts,
+                                  uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
+                                  uint64_t *d_needed, void *d_workspace, uint64_t workspace_bytes,
+                                  void *stream);
+
+/* Wait for `stream` and return (and clear) the latched device status. */
+fmx_status fmx_sync(fmx_index *ix, void *stream);
+
+/* --------------------------------------------------------------- timing
+ * When enabled, every kernel launch is bracketed by hipEvents on its stream;
+ * fmx_timing_read sums their durations per kernel (it synchronises). */
+fmx_status fmx_timing_enable(fmx_index *ix, int enable);
+fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entries, int *n_entries);
+
+/* --------------------------------------------------------------- builder
+ * FmIndexBuilder (src/builder/mod.rs): blob_size (:165-181) and build (:187-264),
+ * on the GPU.  kmer_size 1 = LookupTableConfig::None, >= 2 = KmerSize(k);
+ * sampling_ratio 1 = SuffixArrayConfig::Uncompressed, >= 2 = Compressed(r).
+ * table: 256-byte EncodingTable (host memory), or NULL for PassThrough. */
+fmx_status fmx_build_blob_size(uint64_t text_len, uint32_t symbol_count, fmx_layout layout,
+                               uint32_t kmer_size, uint32_t sampling_ratio, uint64_t *out_size);
+
+/* d_text and d_blob are device buffers on `device`; d_blob must be 16-B aligned
+ * and exactly fmx_build_blob_size bytes.  Synchronous. */
+fmx_status fmx_build_device(const uint8_t *d_text, uint64_t text_len, const uint8_t *table,
+                            uint32_t symbol_count, fmx_layout layout, uint32_t kmer_size,
+                            uint32_t sampling_ratio, uint8_t *d_blob, uint64_t blob_len, int device);
+
+/* Host-buffer convenience: uploads the text, builds on `device`, downloads the blob. */
+fmx_status fmx_build(const uint8_t *text, uint64_t text_len, const uint8_t *table,
+                     uint32_t symbol_count, fmx_layout layout, uint32_t kmer_size,
+                     uint32_t sampling_ratio, uint8_t *blob, uint64_t blob_len, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMX_H */

@@ -1,0 +1,642 @@
+// fmx_api.cpp — the C ABI (include/fmx.h): blob validation, HBM residency,
+// batch orchestration, timing.  Host side of the MI355X engine.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "fmx_internal.hpp"
+
+namespace fmx {
+
+static uint64_t align_up(uint64_t raw, uint64_t a) {
+    const uint64_t r = raw % a;
+    return r == 0 ? raw : raw + (a - r);
+}
+
+static bool layout_valid(const fmx_layout &L) {
+    return (L.pos_bytes == 4 || L.pos_bytes == 8) && L.planes >= 2 && L.planes <= 6 &&
+           (L.vec_bits == 32 || L.vec_bits == 64 || L.vec_bits == 128) &&
+           (L.encoder == FMX_ENC_TABLE || L.encoder == FMX_ENC_PASS);
+}
+
+// Vector::ALIGN_SIZE (blocks/vector.rs:16,31,46): 8 for u32/u64, 16 for u128.
+static uint64_t align_of(const fmx_layout &L) { return L.vec_bits == 128 ? 16 : 8; }
+
+static uint64_t read_p(const uint8_t *p, uint32_t pb) {
+    if (pb == 4) { uint32_t v; memcpy(&v, p, 4); return v; }
+    uint64_t v; memcpy(&v, p, 8); return v;
+}
+
+// FmIndex::load's header walk and exact body-size check
+// (src/load_from_blob.rs:28-58; Header::read_from_blob, components/mod.rs:18-22;
+// MagicNumber::is_valid/is_supported_version, magic_number.rs:38-47), plus the
+// consistency checks that the reference gets from its type parameters.
+fmx_status parse_blob(const BlobReader &rd, uint64_t len, fmx_layout L, BlobView *bv,
+                      uint64_t *expected_total, uint64_t *actual_total) {
+    if (!layout_valid(L)) return FMX_E_LAYOUT;
+    const uint64_t A = align_of(L), pb = L.pos_bytes;
+    BlobView &v = *bv;
+    v = BlobView{};
+    v.L = L;
+    v.align = (uint32_t)A;
+    v.bl = L.vec_bits;
+    v.block_bytes = L.planes * L.vec_bits / 8;
+
+    uint8_t hdr[8 + 256 + 32 + 16 + 32];
+    const uint64_t want = std::min<uint64_t>(len, sizeof(hdr));
+    if (want < 8 || !rd(0, want, hdr)) return FMX_E_FORMAT;
+    if (!(hdr[0] == 'F' && hdr[1] == 'I' && hdr[2] == '0' && hdr[3] == '0')) return FMX_E_FORMAT;
+    uint64_t off = align_up(8, A);
+    if (L.encoder == FMX_ENC_TABLE) {
+        if (off + 256 > want) return FMX_E_FORMAT;
+        memcpy(v.enc, hdr + off, 256);
+        off += align_up(256, A);
+    } else {
+        for (int i = 0; i < 256; ++i) v.enc[i] = (uint8_t)i;  // PassThrough::idx_of
+    }
+    auto u32at = [&](uint64_t o) { uint32_t x; memcpy(&x, hdr + o, 4); return x; };
+    auto u64at = [&](uint64_t o) { uint64_t x; memcpy(&x, hdr + o, 8); return x; };
+    if (off + 24 > want) return FMX_E_FORMAT;
+    const uint32_t ca_sigma = u32at(off), ca_k = u32at(off + 4), ca_len = u32at(off + 8),
+                   mult_len = u32at(off + 12);
+    const uint64_t kt_len = u64at(off + 16);
+    off += align_up(24, A);
+    if (off + 16 > want) return FMX_E_FORMAT;
+    const uint32_t sr = u32at(off);
+    const uint64_t sa_len = u64at(off + 8);
+    off += align_up(16, A);
+    if (off + 24 > want) return FMX_E_FORMAT;
+    const uint32_t bw_sigma = u32at(off);
+    const uint64_t ckpt_len = u64at(off + 8), blocks_len = u64at(off + 16);
+    off += align_up(24, A);
+    v.header_size = off;
+
+    if (ca_len > (1u << 20) || mult_len > 64 || kt_len > (1ull << 40) || sa_len > (1ull << 40) ||
+        ckpt_len > (1ull << 46) || blocks_len > (1ull << 40))
+        return FMX_E_LAYOUT;
+    const uint64_t body_ca = align_up((uint64_t)ca_len * pb, A) + align_up((uint64_t)mult_len * 8, A) +
+                             align_up(kt_len * pb, A);
+    const uint64_t body_sa = align_up(sa_len * pb, A);
+    const uint64_t body_bwm = align_up(pb, A) + align_up(ckpt_len * pb, A) + align_up(blocks_len * v.block_bytes, A);
+    v.total = v.header_size + body_ca + body_sa + body_bwm;
+    if (expected_total) *expected_total = v.total;
+    if (actual_total) *actual_total = len;
+    if (len != v.total) return FMX_E_SIZE;  // LoadError::MismatchedBlobSize
+
+    v.off_ca = v.header_size;
+    v.off_mult = v.off_ca + align_up((uint64_t)ca_len * pb, A);
+    v.off_kmer = v.off_mult + align_up((uint64_t)mult_len * 8, A);
+    v.off_sa = v.off_kmer + align_up(kt_len * pb, A);
+    v.off_sent = v.off_sa + body_sa;
+    v.off_ckpt = v.off_sent + align_up(pb, A);
+    v.off_blocks = v.off_ckpt + align_up(ckpt_len * pb, A);
+
+    if (ca_sigma == 0 || ca_sigma > (uint32_t)kMaxSigma || ca_sigma > (1u << L.planes)) return FMX_E_LAYOUT;
+    if (ca_sigma != bw_sigma || ca_len != ca_sigma + 1 || mult_len != ca_k || ca_k == 0 ||
+        ca_k > (uint32_t)kMaxK || sr == 0)
+        return FMX_E_LAYOUT;
+    v.sigma = ca_sigma; v.k = ca_k; v.sr = sr;
+    uint8_t small[(kMaxSigma + 1) * 8];
+    if (!rd(v.off_ca, (uint64_t)ca_len * pb, small)) return FMX_E_FORMAT;
+    for (uint32_t c = 0; c <= ca_sigma; ++c) v.C[c] = read_p(small + c * pb, (uint32_t)pb);
+    v.n = v.C[ca_sigma];
+    const uint64_t W = ca_sigma + 1;
+    uint64_t wk = 1;
+    for (uint32_t i = 0; i < ca_k; ++i) {
+        if (wk > (1ull << 40) / W) return FMX_E_LAYOUT;
+        wk *= W;
+    }
+    if (kt_len != wk) return FMX_E_LAYOUT;
+    uint64_t mult[kMaxK];
+    if (!rd(v.off_mult, (uint64_t)ca_k * 8, mult)) return FMX_E_FORMAT;
+    uint64_t pw = 1;
+    for (uint32_t i = 0; i < ca_k; ++i) {  // [W^(k-1), .., W^0] (count_array.rs:89-93)
+        if (mult[ca_k - 1 - i] != pw) return FMX_E_LAYOUT;
+        v.mult[ca_k - 1 - i] = pw;
+        pw *= W;
+    }
+    if (blocks_len != v.n / v.bl + 1 || ckpt_len != blocks_len * ca_sigma) return FMX_E_LAYOUT;
+    if (sa_len != (v.n + sr - 1) / sr) return FMX_E_LAYOUT;
+    uint8_t sent[8];
+    if (!rd(v.off_sent, pb, sent)) return FMX_E_FORMAT;
+    v.sentinel = read_p(sent, (uint32_t)pb);
+    if (v.n > 0 && (v.sentinel == 0 || v.sentinel > v.n)) return FMX_E_LAYOUT;
+    if (pb == 4 && v.n >= 0xFFFFFFFFull) return FMX_E_LAYOUT;
+    v.kmer_len = kt_len; v.sa_len = sa_len; v.ckpt_len = ckpt_len; v.blocks_len = blocks_len;
+    return FMX_OK;
+}
+
+// FmIndexBuilder::blob_size (builder/mod.rs:165-181) with the headers of
+// CountArrayHeader::new (count_array.rs:57-77), SuffixArrayHeader::new
+// (suffix_array/mod.rs:43-56), BwmHeader::new (bwm/mod.rs:69-90).
+fmx_status blob_sizes(uint64_t n, uint32_t sigma, fmx_layout L, uint32_t k, uint32_t sr, BlobSizes *S) {
+    if (!layout_valid(L)) return FMX_E_LAYOUT;
+    if (sigma == 0 || sigma > (1u << L.planes)) return FMX_E_SYMBOL;  // BuildError::SymbolCountOver
+    if (k == 0 || sr == 0 || k > (uint32_t)kMaxK) return FMX_E_CONFIG;
+    const uint64_t A = align_of(L), pb = L.pos_bytes, W = sigma + 1;
+    uint64_t wk = 1;
+    for (uint32_t i = 0; i < k; ++i) {
+        wk *= W;
+        if (wk > 0xFFFFFFFFull) return FMX_E_CONFIG;  // u32 pow overflow (count_array.rs:68)
+    }
+    if (pb == 4 && n >= 0xFFFFFFFFull) return FMX_E_CONFIG;
+    S->magic = align_up(8, A);
+    S->enc = L.encoder == FMX_ENC_TABLE ? align_up(256, A) : 0;
+    S->cah = align_up(24, A);
+    S->sah = align_up(16, A);
+    S->bwh = align_up(24, A);
+    S->header = S->magic + S->enc + S->cah + S->sah + S->bwh;
+    S->ca = align_up(W * pb, A);
+    S->mult = align_up((uint64_t)k * 8, A);
+    S->kt_len = wk;
+    S->kt = align_up(wk * pb, A);
+    S->sa_len = (n + sr - 1) / sr;
+    S->sa = align_up(S->sa_len * pb, A);
+    S->sent = align_up(pb, A);
+    S->blocks_len = n / L.vec_bits + 1;
+    S->ckpt_len = S->blocks_len * sigma;
+    S->ckpt = align_up(S->ckpt_len * pb, A);
+    S->blocks = align_up(S->blocks_len * L.planes * (L.vec_bits / 8), A);
+    S->total = S->header + S->ca + S->mult + S->kt + S->sa + S->sent + S->ckpt + S->blocks;
+    return FMX_OK;
+}
+
+// --------------------------------------------------------------- helpers
+
+static hipEvent_t take_event(fmx_index *ix) {
+    if (!ix->event_pool.empty()) {
+        hipEvent_t e = ix->event_pool.back();
+        ix->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+static Timer &timer(fmx_index *ix, const char *name) {
+    for (auto &t : ix->timers)
+        if (t.name == name) return t;
+    ix->timers.push_back(Timer{});
+    ix->timers.back().name = name;
+    return ix->timers.back();
+}
+
+// Bracket one launch with events on its stream when timing is on.
+template <class F>
+static hipError_t timed(fmx_index *ix, const char *name, hipStream_t s, uint64_t units, F &&launch) {
+    if (!ix->timing) return launch();
+    hipEvent_t a = take_event(ix), b = take_event(ix);
+    if (!a || !b) return hipErrorOutOfMemory;
+    hipEventRecord(a, s);
+    hipError_t e = launch();
+    hipEventRecord(b, s);
+    Timer &t = timer(ix, name);
+    t.pending.emplace_back(a, b);
+    t.pending_units.push_back(units);
+    return e;
+}
+
+static fmx_status dev_err(hipError_t e) { return e == hipSuccess ? FMX_OK : FMX_E_DEVICE; }
+
+static fmx_status ensure_scratch(fmx_index *ix, uint64_t bytes) {
+    if (ix->scratch_bytes >= bytes) return FMX_OK;
+    if (ix->d_scratch) hipFree(ix->d_scratch);
+    ix->d_scratch = nullptr;
+    ix->scratch_bytes = 0;
+    const uint64_t want = std::max<uint64_t>(bytes, 1 << 20);
+    if (hipMalloc(&ix->d_scratch, want) != hipSuccess) return FMX_E_DEVICE;
+    ix->scratch_bytes = want;
+    return FMX_OK;
+}
+
+static fmx_status finish_load(fmx_index *ix, uint32_t occ_mode) {
+    QueryArgs &q = ix->qa;
+    const BlobView &v = ix->bv;
+    q = QueryArgs{};
+    q.ckpt = ix->d_blob + v.off_ckpt;
+    q.blocks = ix->d_blob + v.off_blocks;
+    q.sa = ix->d_blob + v.off_sa;
+    q.kmer = ix->d_blob + v.off_kmer;
+    q.n = v.n;
+    q.sentinel = v.sentinel;
+    q.sigma = v.sigma;
+    q.k = v.k;
+    q.sr = v.sr;
+    q.sr_pow2_mask = (v.sr > 1 && (v.sr & (v.sr - 1)) == 0) ? v.sr - 1 : 0;
+    q.strict = v.L.encoder == FMX_ENC_PASS;
+    memcpy(q.C, v.C, sizeof(q.C));
+    memcpy(q.mult, v.mult, sizeof(q.mult));
+    memcpy(q.enc, v.enc, 256);
+    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMalloc(&ix->d_status, 64) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMemset(ix->d_status, 0, 64) != hipSuccess) return FMX_E_DEVICE;
+    q.status = ix->d_status;
+    ix->occ_mode = FMX_OCC_BLOB;
+    if (occ_mode == FMX_OCC_INTERLEAVED) {
+        const uint32_t rec = interleaved_record_bytes(v);
+        if (rec != 0) {
+            ix->rec_bytes = rec;
+            ix->occ_bytes = v.blocks_len * rec;
+            if (hipMalloc(&ix->d_occ, ix->occ_bytes) != hipSuccess) return FMX_E_DEVICE;
+            q.occ = ix->d_occ;
+            q.rec_bytes = rec;
+            ix->occ_mode = FMX_OCC_INTERLEAVED;
+            if (launch_relayout(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+            if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
+        }
+    }
+    return FMX_OK;
+}
+
+static fmx_status read_status(fmx_index *ix, hipStream_t s) {
+    uint32_t st = 0;
+    if (hipMemcpyAsync(&st, ix->d_status, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
+    if (hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
+    if (st) {
+        hipMemsetAsync(ix->d_status, 0, 4, s);
+        hipStreamSynchronize(s);
+    }
+    if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
+    if (st & kStatusSymbol) return FMX_E_SYMBOL;
+    return FMX_OK;
+}
+
+}  // namespace fmx
+
+using namespace fmx;
+
+// =================================================================== C ABI
+
+extern "C" {
+
+uint32_t fmx_abi_version(void) { return FMX_ABI_VERSION; }
+
+const char *fmx_status_str(fmx_status s) {
+    switch (s) {
+        case FMX_OK: return "ok";
+        case FMX_E_FORMAT: return "invalid FM-index format";
+        case FMX_E_SIZE: return "mismatched blob size";
+        case FMX_E_ALIGN: return "misaligned blob";
+        case FMX_E_LAYOUT: return "layout does not match blob";
+        case FMX_E_EMPTY_PATTERN: return "empty pattern";
+        case FMX_E_SYMBOL: return "symbol out of range";
+        case FMX_E_CAPACITY: return "output capacity too small";
+        case FMX_E_DEVICE: return "device error";
+        case FMX_E_ARG: return "invalid argument";
+        case FMX_E_CONFIG: return "invalid build configuration";
+    }
+    return "unknown";
+}
+
+int fmx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, int device, uint32_t occ_mode,
+                    fmx_index **out, uint64_t *expected_total, uint64_t *actual_total) {
+    if (!out || (!blob && blob_len)) return FMX_E_ARG;
+    *out = nullptr;
+    if (!layout_valid(layout)) return FMX_E_LAYOUT;
+    if (((uintptr_t)blob) % align_of(layout) != 0) return FMX_E_ALIGN;  // zerocopy alignment panic
+    BlobView bv;
+    BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
+        if (off + len > blob_len) return false;
+        memcpy(dst, blob + off, len);
+        return true;
+    };
+    fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
+    if (st) return st;
+    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    fmx_index *ix = new (std::nothrow) fmx_index();
+    if (!ix) return FMX_E_DEVICE;
+    ix->bv = bv;
+    ix->device = device;
+    ix->host_blob = blob;
+    ix->blob_len = blob_len;
+    if (hipMalloc(&ix->d_blob_owned, blob_len) != hipSuccess ||
+        hipMemcpy(ix->d_blob_owned, blob, blob_len, hipMemcpyHostToDevice) != hipSuccess) {
+        fmx_free(ix);
+        return FMX_E_DEVICE;
+    }
+    ix->d_blob = ix->d_blob_owned;
+    st = finish_load(ix, occ_mode);
+    if (st) { fmx_free(ix); return st; }
+    *out = ix;
+    return FMX_OK;
+}
+
+fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout layout, int device,
+                           uint32_t occ_mode, fmx_index **out, uint64_t *expected_total, uint64_t *actual_total) {
+    if (!out || !d_blob) return FMX_E_ARG;
+    *out = nullptr;
+    if (!layout_valid(layout)) return FMX_E_LAYOUT;
+    if (((uintptr_t)d_blob) % align_of(layout) != 0) return FMX_E_ALIGN;
+    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    BlobView bv;
+    BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
+        if (off + len > blob_len) return false;
+        return hipMemcpy(dst, d_blob + off, len, hipMemcpyDeviceToHost) == hipSuccess;
+    };
+    fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
+    if (st) return st;
+    fmx_index *ix = new (std::nothrow) fmx_index();
+    if (!ix) return FMX_E_DEVICE;
+    ix->bv = bv;
+    ix->device = device;
+    ix->blob_len = blob_len;
+    ix->d_blob = d_blob;
+    st = finish_load(ix, occ_mode);
+    if (st) { fmx_free(ix); return st; }
+    *out = ix;
+    return FMX_OK;
+}
+
+void fmx_free(fmx_index *ix) {
+    if (!ix) return;
+    hipSetDevice(ix->device);
+    if (ix->stream) hipStreamSynchronize(ix->stream);
+    for (auto &t : ix->timers)
+        for (auto &p : t.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+    for (auto e : ix->event_pool) hipEventDestroy(e);
+    if (ix->d_scratch) hipFree(ix->d_scratch);
+    if (ix->d_occ) hipFree(ix->d_occ);
+    if (ix->d_status) hipFree(ix->d_status);
+    if (ix->d_blob_owned) hipFree(ix->d_blob_owned);
+    if (ix->stream) hipStreamDestroy(ix->stream);
+    delete ix;
+}
+
+const uint8_t *fmx_blob(const fmx_index *ix, uint64_t *len) {
+    if (!ix) return nullptr;
+    if (len) *len = ix->host_blob ? ix->blob_len : 0;
+    return ix->host_blob;
+}
+
+fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
+    if (!ix || !o) return FMX_E_ARG;
+    memset(o, 0, sizeof(*o));
+    o->text_len = ix->bv.n;
+    o->sentinel_index = ix->bv.sentinel;
+    o->blob_len = ix->blob_len;
+    o->device_bytes = (ix->d_blob_owned ? ix->blob_len : 0) + ix->occ_bytes;
+    o->symbol_count = ix->bv.sigma;
+    o->kmer_size = ix->bv.k;
+    o->sampling_ratio = ix->bv.sr;
+    o->block_len = ix->bv.bl;
+    o->occ_mode = ix->occ_mode;
+    o->device = ix->device;
+    return FMX_OK;
+}
+
+// ---------------------------------------------------------------- async
+
+fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                                 uint32_t flags, void *d_counts, void *stream) {
+    if (!ix || (n && (!d_bytes || !d_offsets || !d_counts))) return FMX_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    return dev_err(timed(ix, "count", s, n, [&] {
+        return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, nullptr, nullptr, s);
+    }));
+}
+
+static uint64_t ws_layout(const fmx_index *ix, uint64_t n, uint64_t *o_cnt, uint64_t *o_lo, uint64_t *o_tmp,
+                          size_t *tmp_bytes) {
+    size_t tb = 0;
+    scan_workspace_bytes(n, &tb);
+    *tmp_bytes = tb;
+    *o_cnt = 0;
+    *o_lo = align_up((n + 1) * 8, 256);
+    *o_tmp = *o_lo + align_up(std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes, 256);
+    return *o_tmp + align_up(tb, 256);
+}
+
+fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {
+    if (!ix || !bytes) return FMX_E_ARG;
+    uint64_t a, b, c;
+    size_t t;
+    *bytes = ws_layout(ix, n, &a, &b, &c, &t);
+    return FMX_OK;
+}
+
+fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                                  uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs,
+                                  uint64_t cap, uint64_t *d_needed, void *d_ws, uint64_t ws_bytes, void *stream) {
+    if (!ix || !d_loc_offsets || (n && (!d_bytes || !d_offsets)) || (cap && !d_locs)) return FMX_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    uint64_t o_cnt, o_lo, o_tmp;
+    size_t tb;
+    const uint64_t need = ws_layout(ix, n, &o_cnt, &o_lo, &o_tmp, &tb);
+    if (!d_ws || ws_bytes < need) return FMX_E_ARG;
+    uint8_t *ws = (uint8_t *)d_ws;
+    uint64_t *cnt64 = (uint64_t *)(ws + o_cnt);
+    void *lo = ws + o_lo;
+    hipError_t e = hipMemsetAsync(cnt64 + n, 0, 8, s);
+    if (e == hipSuccess)
+        e = timed(ix, "count", s, n, [&] {
+            return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, cnt64, lo, s);
+        });
+    if (e == hipSuccess)
+        e = timed(ix, "scan", s, n, [&] { return launch_scan(cnt64, d_loc_offsets, n + 1, ws + o_tmp, tb, s); });
+    if (e == hipSuccess && d_needed)
+        e = hipMemcpyAsync(d_needed, d_loc_offsets + n, 8, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess)
+        e = timed(ix, "locate", s, n, [&] { return launch_locate(ix, d_loc_offsets, lo, n, d_locs, cap, s); });
+    return dev_err(e);
+}
+
+fmx_status fmx_sync(fmx_index *ix, void *stream) {
+    if (!ix) return FMX_E_ARG;
+    return read_status(ix, stream ? (hipStream_t)stream : ix->stream);
+}
+
+// ----------------------------------------------------------- host buffers
+
+static fmx_status check_patterns(const uint64_t *offsets, uint64_t n) {
+    if (n && offsets[0] != 0) return FMX_E_ARG;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) return FMX_E_ARG;
+        if (offsets[i + 1] == offsets[i]) return FMX_E_EMPTY_PATTERN;  // count_array.rs:211 panics
+    }
+    return FMX_OK;
+}
+
+fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets, uint64_t n,
+                           uint32_t flags, void *out_counts) {
+    if (!ix || (n && (!offsets || !out_counts))) return FMX_E_ARG;
+    if (n == 0) return FMX_OK;
+    std::lock_guard<std::mutex> g(ix->mu);
+    fmx_status st = check_patterns(offsets, n);
+    if (st) return st;
+    hipSetDevice(ix->device);
+    const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
+    const uint64_t o_off = align_up(nb, 256), o_cnt = o_off + align_up((n + 1) * 8, 256);
+    st = ensure_scratch(ix, o_cnt + n * pb);
+    if (st) return st;
+    hipStream_t s = ix->stream;
+    uint8_t *d = ix->d_scratch;
+    hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return FMX_E_DEVICE;
+    st = fmx_count_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, d + o_cnt, s);
+    if (st) return st;
+    if (hipMemcpyAsync(out_counts, d + o_cnt, n * pb, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
+    return read_status(ix, s);
+}
+
+fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets, uint64_t n,
+                            uint32_t flags, uint64_t *out_loc_offsets, void *out_locs, uint64_t cap,
+                            uint64_t *needed) {
+    if (!ix || !out_loc_offsets || (n && !offsets) || (cap && !out_locs)) return FMX_E_ARG;
+    if (needed) *needed = 0;
+    if (n == 0) { out_loc_offsets[0] = 0; return FMX_OK; }
+    std::lock_guard<std::mutex> g(ix->mu);
+    fmx_status st = check_patterns(offsets, n);
+    if (st) return st;
+    hipSetDevice(ix->device);
+    const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
+    uint64_t o_cnt, o_lo, o_tmp;
+    size_t tb;
+    const uint64_t wsb = ws_layout(ix, n, &o_cnt, &o_lo, &o_tmp, &tb);
+    const uint64_t o_off = align_up(nb, 256);
+    const uint64_t o_loff = o_off + align_up((n + 1) * 8, 256);
+    const uint64_t o_ws = o_loff + align_up((n + 1) * 8, 256);
+    const uint64_t o_locs = o_ws + align_up(wsb, 256);
+    st = ensure_scratch(ix, o_locs);
+    if (st) return st;
+    hipStream_t s = ix->stream;
+    uint8_t *d = ix->d_scratch;
+    hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
+    // phase 1: SA intervals and their exclusive scan
+    uint8_t *ws = d + o_ws;
+    uint64_t *cnt64 = (uint64_t *)(ws + o_cnt);
+    uint64_t *loff = (uint64_t *)(d + o_loff);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt64 + n, 0, 8, s);
+    if (e == hipSuccess)
+        e = timed(ix, "count", s, n, [&] {
+            return launch_count(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, cnt64, ws + o_lo, s);
+        });
+    if (e == hipSuccess)
+        e = timed(ix, "scan", s, n, [&] { return launch_scan(cnt64, loff, n + 1, ws + o_tmp, tb, s); });
+    if (e == hipSuccess) e = hipMemcpyAsync(out_loc_offsets, loff, (n + 1) * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return FMX_E_DEVICE;
+    st = read_status(ix, s);
+    if (st) return st;
+    const uint64_t total = out_loc_offsets[n];
+    if (needed) *needed = total;
+    if (total > cap) return FMX_E_CAPACITY;
+    // phase 2: the walk, into scratch sized for exactly `total` locations
+    st = ensure_scratch(ix, o_locs + std::max<uint64_t>(total, 1) * pb);
+    if (st) return st;
+    if (ix->d_scratch != d) {  // scratch moved: re-upload what phase 2 reads
+        d = ix->d_scratch;
+        ws = d + o_ws;
+        loff = (uint64_t *)(d + o_loff);
+        // lo[] lived in the old scratch: recompute phase 1 into the new one
+        cnt64 = (uint64_t *)(ws + o_cnt);
+        e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = launch_count(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, cnt64, ws + o_lo, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(loff, out_loc_offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return FMX_E_DEVICE;
+    }
+    e = timed(ix, "locate", s, n, [&] { return launch_locate(ix, loff, ws + o_lo, n, d + o_locs, total, s); });
+    if (e == hipSuccess && total) e = hipMemcpyAsync(out_locs, d + o_locs, total * pb, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return FMX_E_DEVICE;
+    return read_status(ix, s);
+}
+
+// ---------------------------------------------------------------- timing
+
+fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
+    if (!ix) return FMX_E_ARG;
+    ix->timing = enable != 0;
+    return FMX_OK;
+}
+
+fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entries, int *n_entries) {
+    if (!ix || !n_entries) return FMX_E_ARG;
+    for (auto &t : ix->timers) {
+        for (size_t i = 0; i < t.pending.size(); ++i) {
+            auto &p = t.pending[i];
+            if (hipEventSynchronize(p.second) != hipSuccess) return FMX_E_DEVICE;
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, p.first, p.second);
+            t.ms += ms;
+            t.launches += 1;
+            t.units += t.pending_units[i];
+            ix->event_pool.push_back(p.first);
+            ix->event_pool.push_back(p.second);
+        }
+        t.pending.clear();
+        t.pending_units.clear();
+    }
+    int k = 0;
+    for (auto &t : ix->timers) {
+        if (out && k < max_entries) {
+            memset(&out[k], 0, sizeof(out[k]));
+            snprintf(out[k].name, sizeof(out[k].name), "%s", t.name.c_str());
+            out[k].launches = t.launches;
+            out[k].total_ms = t.ms;
+            out[k].units = t.units;
+        }
+        ++k;
+    }
+    *n_entries = k;
+    return FMX_OK;
+}
+
+// --------------------------------------------------------------- builder
+
+fmx_status fmx_build_blob_size(uint64_t text_len, uint32_t symbol_count, fmx_layout layout, uint32_t kmer_size,
+                               uint32_t sampling_ratio, uint64_t *out_size) {
+    if (!out_size) return FMX_E_ARG;
+    BlobSizes S;
+    fmx_status st = blob_sizes(text_len, symbol_count, layout, kmer_size, sampling_ratio, &S);
+    if (st) return st;
+    *out_size = S.total;
+    return FMX_OK;
+}
+
+fmx_status fmx_build_device(const uint8_t *d_text, uint64_t text_len, const uint8_t *table, uint32_t symbol_count,
+                            fmx_layout layout, uint32_t kmer_size, uint32_t sampling_ratio, uint8_t *d_blob,
+                            uint64_t blob_len, int device) {
+    if (!d_blob || (text_len && !d_text)) return FMX_E_ARG;
+    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
+    fmx_status st = build_device(d_text, text_len, table, symbol_count, layout, kmer_size, sampling_ratio, d_blob,
+                                 blob_len, s);
+    hipStreamSynchronize(s);
+    hipStreamDestroy(s);
+    return st;
+}
+
+fmx_status fmx_build(const uint8_t *text, uint64_t text_len, const uint8_t *table, uint32_t symbol_count,
+                     fmx_layout layout, uint32_t kmer_size, uint32_t sampling_ratio, uint8_t *blob,
+                     uint64_t blob_len, int device) {
+    if (!blob || (text_len && !text)) return FMX_E_ARG;
+    if (((uintptr_t)blob) % align_of(layout) != 0) return FMX_E_ALIGN;  // BuildError::NotAlignedBlob
+    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    uint8_t *dt = nullptr, *db = nullptr;
+    if (hipMalloc(&dt, std::max<uint64_t>(text_len, 1)) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMalloc(&db, std::max<uint64_t>(blob_len, 16)) != hipSuccess) { hipFree(dt); return FMX_E_DEVICE; }
+    fmx_status st = FMX_OK;
+    if (text_len && hipMemcpy(dt, text, text_len, hipMemcpyHostToDevice) != hipSuccess) st = FMX_E_DEVICE;
+    if (!st) st = fmx_build_device(dt, text_len, table, symbol_count, layout, kmer_size, sampling_ratio, db,
+                                   blob_len, device);
+    if (!st && hipMemcpy(blob, db, blob_len, hipMemcpyDeviceToHost) != hipSuccess) st = FMX_E_DEVICE;
+    hipFree(dt);
+    hipFree(db);
+    return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// Internal declarations shared by the C-ABI (fmx_api.cpp), the query kernels
+// (fmx_query.hip) and the GPU blob builder (fmx_build.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/fmx.h"
+
+namespace fmx {
+
+constexpr int kMaxSigma = 64;  // Block6 indexes at most 2^6 symbols (blocks/block6.rs:15)
+constexpr int kMaxK = 40;      // W^k must fit the u32 header field anyway (count_array.rs:68)
+
+// Parsed blob headers.  Field-for-field what FmIndex::load derives
+// (src/load_from_blob.rs:28-85); offsets are byte offsets into the blob.
+struct BlobView {
+    fmx_layout L{};
+    uint32_t align = 8, bl = 64, block_bytes = 0;
+    uint32_t sigma = 0, k = 0, sr = 0;
+    uint64_t n = 0, sentinel = 0;
+    uint64_t C[kMaxSigma + 1] = {};
+    uint64_t mult[kMaxK] = {};
+    uint8_t enc[256] = {};
+    uint64_t kmer_len = 0, sa_len = 0, ckpt_len = 0, blocks_len = 0;
+    uint64_t off_ca = 0, off_mult = 0, off_kmer = 0, off_sa = 0, off_sent = 0, off_ckpt = 0,
+             off_blocks = 0;
+    uint64_t header_size = 0, total = 0;
+};
+
+// Reads `len` bytes at blob offset `off` into dst (host or device source).
+using BlobReader = std::function<bool(uint64_t off, uint64_t len, void *dst)>;
+
+fmx_status parse_blob(const BlobReader &rd, uint64_t blob_len, fmx_layout L, BlobView *out,
+                      uint64_t *expected_total, uint64_t *actual_total);
+
+// Blob section sizes for the builder (FmIndexBuilder::blob_size, builder/mod.rs:165-181).
+struct BlobSizes {
+    uint64_t magic, enc, cah, sah, bwh, header;
+    uint64_t ca, mult, kt, kt_len, sa_len, sa, sent, ckpt_len, ckpt, blocks_len, blocks, total;
+};
+fmx_status blob_sizes(uint64_t n, uint32_t sigma, fmx_layout L, uint32_t k, uint32_t sr, BlobSizes *S);
+
+// Kernel arguments for the query kernels (passed by value; < 2 KB).
+struct QueryArgs {
+    const uint8_t *ckpt;      // rank_checkpoints [P; blocks_len * sigma]
+    const uint8_t *blocks;    // blocks [BlockN<V>; blocks_len]
+    const uint8_t *sa;        // sampled suffix array [P; sa_len]
+    const uint8_t *kmer;      // kmer_count_table [P; W^k]
+    const uint8_t *occ;       // interleaved occ records (FMX_OCC_INTERLEAVED), else null
+    uint32_t *status;         // latched device status bits
+    uint64_t n, sentinel;
+    uint32_t sigma, k, sr, sr_pow2_mask;  // sr_pow2_mask = sr-1 if sr is a power of two, else 0
+    uint32_t strict;          // PassThrough: bytes >= sigma are an error
+    uint32_t rec_bytes;       // interleaved record size
+    uint64_t C[kMaxSigma + 1];
+    uint64_t mult[kMaxK];
+    uint8_t enc[256];
+};
+
+// Device status bits
+constexpr uint32_t kStatusEmpty = 1u;
+constexpr uint32_t kStatusSymbol = 2u;
+
+struct Timer {
+    std::string name;
+    uint64_t launches = 0;
+    double ms = 0.0;
+    uint64_t units = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<uint64_t> pending_units;
+};
+
+}  // namespace fmx
+
+struct fmx_index {
+    fmx::BlobView bv;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    const uint8_t *host_blob = nullptr;
+    uint64_t blob_len = 0;
+    uint8_t *d_blob_owned = nullptr;
+    const uint8_t *d_blob = nullptr;
+    uint8_t *d_occ = nullptr;
+    uint64_t occ_bytes = 0;
+    uint32_t occ_mode = FMX_OCC_BLOB;
+    uint32_t rec_bytes = 0;
+    uint32_t *d_status = nullptr;
+    fmx::QueryArgs qa{};
+    // host-API scratch (grown on demand)
+    uint8_t *d_scratch = nullptr;
+    uint64_t scratch_bytes = 0;
+    // timing
+    bool timing = false;
+    std::vector<fmx::Timer> timers;
+    std::vector<hipEvent_t> event_pool;
+    std::mutex mu;
+};
+
+namespace fmx {
+
+// Query launchers (fmx_query.hip).  All asynchronous on `stream`.
+hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
+                        uint64_t n, uint32_t flags, void *d_counts_p, uint64_t *d_counts_u64,
+                        void *d_lo_p, hipStream_t stream);
+hipError_t launch_locate(const fmx_index *ix, const uint64_t *d_loc_offsets, const void *d_lo_p,
+                         uint64_t n, void *d_locs, uint64_t cap, hipStream_t stream);
+hipError_t scan_workspace_bytes(uint64_t n, size_t *bytes);
+hipError_t launch_scan(const uint64_t *d_in, uint64_t *d_out, uint64_t n_plus_1, void *tmp,
+                       size_t tmp_bytes, hipStream_t stream);
+hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
+uint32_t interleaved_record_bytes(const BlobView &bv);
+
+// GPU builder (fmx_build.hip).
+fmx_status build_device(const uint8_t *d_text, uint64_t n, const uint8_t *table, uint32_t sigma,
+                        fmx_layout L, uint32_t k, uint32_t sr, uint8_t *d_blob, uint64_t blob_len,
+                        hipStream_t stream);
+
+}  // namespace fmx

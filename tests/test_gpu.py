@@ -1,0 +1,278 @@
+"""GPU parity tests: every result of the gfx950 kernels is compared bit for bit
+with the oracle (oracle/fmx_oracle.c) on the same inputs — counts, and
+locations element-wise in suffix-array-row order — through the C ABI.
+The GPU blob builder is compared byte for byte with the oracle's builder."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from _util import (ALL_LAYOUTS, encode, occurrences, rand_chr_list, rand_pattern, rand_text,
+                   table_from_symbols)
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+OCC_MODES = ("blob", "interleaved")
+
+
+def block_of(pkg, planes, vb):
+    return getattr(pkg.blocks, f"Block{planes}")(pkg.Vector(vb))
+
+
+def pos_of(pkg, pb):
+    return pkg.u32 if pb == 4 else pkg.u64
+
+
+def gpu_build(pkg, text, sigma, pb, planes, vb, k, sr, table):
+    enc = pkg.text_encoders.EncodingTable(table) if table is not None else pkg.text_encoders.PassThrough()
+    LT = pkg.build_config.LookupTableConfig.KmerSize(k) if k > 1 else pkg.build_config.LookupTableConfig.None_()
+    SA = pkg.build_config.SuffixArrayConfig.Compressed(sr) if sr > 1 else pkg.build_config.SuffixArrayConfig.Uncompressed()
+    b = (pkg.FmIndexBuilder(len(text), sigma, enc, pos_of(pkg, pb), block_of(pkg, planes, vb))
+         .set_lookup_table_config(LT).set_suffix_array_config(SA))
+    blob = pkg.aligned_buffer(b.blob_size())
+    b.build(np.frombuffer(bytes(text), np.uint8), blob)
+    return blob
+
+
+def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True):
+    L = O.layout(pb, planes, vb, enc)
+    orc = O.OracleIndex(blob, L)
+    encoder = pkg.text_encoders.EncodingTable if enc == 0 else pkg.text_encoders.PassThrough
+    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, occ=occ)
+    data, offsets = pkg.pack_patterns(pats)
+    ooff, olocs = orc.locate_batch(data, offsets)
+    goff, glocs = ix.locate_batch((data, offsets))
+    assert np.array_equal(goff, ooff), "per-pattern counts / offsets differ"
+    assert np.array_equal(glocs, olocs), "locations differ (SA-row order)"
+    cnt = ix.count_batch((data, offsets))
+    assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff))
+    if reversed_too:
+        rpats = [p[::-1] for p in pats]
+        rc = ix.count_batch(rpats, reversed=True)
+        assert np.array_equal(rc, cnt)
+        roff, rlocs = ix.locate_batch(rpats, reversed=True)
+        assert np.array_equal(roff, ooff) and np.array_equal(rlocs, olocs)
+    ix.close()
+    return ooff, olocs
+
+
+def test_readme_known_answers_gpu(pkg, O):
+    g = json.load(open(os.path.join(HERE, "golden", "readme.json")))
+    table = pkg.text_encoders.EncodingTable.from_symbols([s.encode() for s in g["symbols"]])
+    b = pkg.FmIndexBuilder(len(g["text"]), table.symbol_count(), table, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64))
+    blob = pkg.aligned_buffer(b.blob_size())
+    b.build(g["text"].encode(), blob)
+    for occ in OCC_MODES:
+        fm = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64), pkg.text_encoders.EncodingTable,
+                              occ=occ)
+        for case in g["cases"]:
+            p = case["pattern"].encode()
+            if "count" in case:
+                assert fm.count(p) == case["count"]
+            assert sorted(fm.locate(p)) == case["sorted_locations"]
+        buf = [7]
+        fm.locate_to_buffer(b"TA", buf)  # appends (locate/mod.rs:28,35)
+        assert buf[0] == 7 and sorted(buf[1:]) == [5, 18]
+        assert fm.count_rev_iter(iter(b"AT")) == 2
+        fm.close()
+
+
+def test_golden_blobs_on_gpu(pkg, O):
+    """The committed golden blobs: GPU builder reproduces them, kernels answer them."""
+    g = json.load(open(os.path.join(HERE, "golden", "oracle_cases.json")))
+    for c in g["cases"]:
+        pb, planes, vb = c["layout"]
+        text, table = bytes.fromhex(c["text"]), bytes.fromhex(c["table"])
+        blob = gpu_build(pkg, text, c["sigma"], pb, planes, vb, c["kmer_size"], c["sampling_ratio"], table)
+        assert bytes(blob).hex() == c["blob"]
+        for occ in OCC_MODES:
+            ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), occ=occ)
+            for q in c["queries"]:
+                p = bytes.fromhex(q["pattern"])
+                assert ix.count(p) == q["count"]
+                assert ix.locate(p) == q["locations"]
+            ix.close()
+
+
+@pytest.mark.parametrize("pb,planes,vb", ALL_LAYOUTS)
+def test_builder_and_queries_every_layout(pkg, O, pb, planes, vb):
+    """get_accurate_result-style sweep on the GPU: builder bytes, then count and
+    locate against the oracle for both device occ layouts."""
+    rng = np.random.default_rng(pb * 1000 + planes * 100 + vb)
+    for sigma in sorted({2, 3, (1 << planes) // 2 + 1, 1 << planes}):
+        chars = rand_chr_list(rng, sigma)
+        table = table_from_symbols([bytes([c]) for c in chars])
+        text = rand_text(rng, chars, 300, 2000)
+        k, sr = int(rng.integers(1, 5)), int(rng.integers(1, 5))
+        if (sigma + 1) ** k > 1 << 20:
+            k = 2
+        blob = gpu_build(pkg, text, sigma, pb, planes, vb, k, sr, table)
+        ref = O.build(text, sigma, O.layout(pb, planes, vb), k, sr, table)
+        assert np.array_equal(blob, ref), f"builder differs sigma={sigma} k={k} sr={sr}"
+        pats = [rand_pattern(rng, text, 1, 24) for _ in range(300)]
+        pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=int(rng.integers(1, 12))))
+                 for _ in range(50)]                              # mostly absent
+        pats += [b"\x00", b"\x7f\x7f", chars[:1] * 2]              # wildcard bytes, short repeats
+        for occ in OCC_MODES:
+            check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+
+
+@pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 64, 127, 128, 129, 4096])
+def test_block_boundaries(pkg, O, n):
+    """n % BLOCK_LEN == 0 appends a zero block + checkpoint row (bwm/mod.rs:136-142)."""
+    rng = np.random.default_rng(n)
+    table = table_from_symbols([b"A", b"C", b"G", b"T"])
+    text = bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=n)) if n else b""
+    for pb, planes, vb in [(4, 2, 32), (8, 2, 64), (4, 3, 128), (8, 6, 128)]:
+        for k, sr in [(1, 1), (3, 2), (4, 3)]:
+            blob = gpu_build(pkg, text, 4, pb, planes, vb, k, sr, table)
+            assert np.array_equal(blob, O.build(text, 4, O.layout(pb, planes, vb), k, sr, table))
+            pats = [b"A", b"AC", b"ACG", b"ACGT", b"T", b"NN", b"GATTACA"] + \
+                   ([text[i:i + 5] for i in range(0, max(n - 5, 0), 7)] if n > 5 else [])
+            for occ in OCC_MODES:
+                check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+
+
+def test_pass_through(pkg, O):
+    """PassThrough encoder (pass_through.rs): text and patterns are indices."""
+    rng = np.random.default_rng(11)
+    for sigma, planes in [(2, 2), (3, 2), (7, 3), (30, 5)]:
+        text = bytes(rng.integers(0, sigma, size=3000).astype(np.uint8))
+        blob = gpu_build(pkg, text, sigma, 4, planes, 64, 3, 2, None)
+        assert np.array_equal(blob, O.build(text, sigma, O.layout(4, planes, 64), 3, 2, None))
+        pats = [rand_pattern(rng, text, 1, 15) for _ in range(200)]
+        for occ in OCC_MODES:
+            check_parity(pkg, O, blob, 4, planes, 64, 1, pats, occ)
+
+
+def test_high_count_patterns(pkg, O):
+    """Skewed occurrence counts: one pattern with ~all rows, many with few —
+    exercises the wave-level row balancing of k_locate."""
+    text = (b"AC" * 20000) + b"GT" * 50 + (b"A" * 5000)
+    table = table_from_symbols([b"A", b"C", b"G", b"T"])
+    for pb, planes, vb in [(4, 2, 64), (8, 3, 128)]:
+        blob = gpu_build(pkg, text, 4, pb, planes, vb, 3, 3, table)
+        pats = [b"A", b"AC", b"CA", b"ACA", b"G", b"GT", b"TA", b"AAAA"] * 20 + [b"C"]
+        for occ in OCC_MODES:
+            ooff, _ = check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+        t_idx = encode(table, text)
+        assert int(ooff[1] - ooff[0]) == len(occurrences(t_idx, b"\x00"))
+
+
+def test_repetitive_text_builder(pkg, O):
+    """Worst case for prefix doubling: long runs need many doubling rounds."""
+    rng = np.random.default_rng(3)
+    table = table_from_symbols([b"A", b"C", b"G", b"T"])
+    text = b"A" * 30000 + bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=500)) + b"ACGT" * 5000
+    blob = gpu_build(pkg, text, 4, 4, 2, 64, 3, 2, table)
+    assert np.array_equal(blob, O.build(text, 4, O.layout(4, 2, 64), 3, 2, table))
+    check_parity(pkg, O, blob, 4, 2, 64, 0, [b"A" * 17, b"ACGTA", b"AAAC", b"TA"], "interleaved")
+
+
+def test_c1_config(pkg, O):
+    """BASELINE configs[0]: 1 Mbp ACGT (T wildcard), u32/Block2<u64>, sr 2,
+    k 3, 1,000 x 20 bp patterns — builder bytes and every result."""
+    rng = np.random.default_rng(42)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=1_000_000).astype(np.uint8)
+    table = table_from_symbols([b"Aa", b"Cc", b"Gg", b"Tt"])
+    blob = gpu_build(pkg, text.tobytes(), 4, 4, 2, 64, 3, 2, table)
+    assert blob.size == 2_500_920
+    ref = O.build(text.tobytes(), 4, O.layout(4, 2, 64), 3, 2, table)
+    assert np.array_equal(blob, ref)
+    starts = rng.integers(0, text.size - 20, size=1000)
+    pats = [text[s:s + 20].tobytes() for s in starts]
+    for occ in OCC_MODES:
+        ooff, olocs = check_parity(pkg, O, blob, 4, 2, 64, 0, pats, occ, reversed_too=False)
+    # every pattern was cut from the text: its start must be among its locations
+    for i, s in enumerate(starts):
+        assert int(s) in set(int(x) for x in olocs[ooff[i]:ooff[i + 1]])
+
+
+def test_errors_gpu(pkg, O):
+    table = table_from_symbols([b"A", b"C", b"G", b"T"])
+    blob = gpu_build(pkg, b"ACGTACGTAC", 4, 4, 2, 64, 2, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64))
+    with pytest.raises(pkg.FmxError) as e:
+        ix.count_batch([b"AC", b""])
+    assert e.value.code == pkg._native.FMX_E_EMPTY_PATTERN
+    assert ix.count(b"AC") == 3  # the index stays usable
+    pt_blob = gpu_build(pkg, bytes([0, 1, 2, 3, 0, 1]), 4, 4, 2, 64, 1, 1, None)
+    pt = pkg.FmIndex.load(pt_blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64), pkg.text_encoders.PassThrough)
+    with pytest.raises(pkg.FmxError) as e:
+        pt.count(bytes([0, 4]))
+    assert e.value.code == pkg._native.FMX_E_SYMBOL
+    assert pt.count(bytes([0, 1])) == 2
+    with pytest.raises(pkg.FmxError):
+        gpu_build(pkg, b"ACGQ", 3, 4, 2, 64, 1, 1, bytes([5] * 256))  # idx 5 >= symbol_count 3
+
+
+def test_device_async_api(pkg, O):
+    """fmx_count_batch_async / fmx_locate_batch_async on HBM-resident buffers
+    (torch tensors as plumbing) give the host API's results."""
+    import torch
+    rng = np.random.default_rng(9)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    starts = rng.integers(0, text.size - 20, size=5000)
+    pats = [text[s:s + 20].tobytes() for s in starts]
+    data, offsets = pkg.pack_patterns(pats)
+    hoff, hlocs = ix.locate_batch((data, offsets))
+    dev = torch.device("cuda:0")
+    d_data = torch.from_numpy(data.copy()).to(dev)
+    d_off = torch.from_numpy(offsets.view(np.int64).copy()).to(dev)
+    n = len(pats)
+    d_cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_loff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    cap = int(hlocs.size) + 16
+    d_locs = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_need = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = ix.locate_workspace_size(n)
+    d_ws = torch.empty(ws, dtype=torch.uint8, device=dev)
+    ix.locate_batch_async(d_data.data_ptr(), d_off.data_ptr(), n, d_loff.data_ptr(), d_locs.data_ptr(), cap,
+                          d_need.data_ptr(), d_ws.data_ptr(), ws, d_counts=d_cnt.data_ptr())
+    ix.sync()
+    assert int(d_need.item()) == hlocs.size
+    assert np.array_equal(d_loff.cpu().numpy().view(np.uint64), hoff)
+    assert np.array_equal(d_locs.cpu().numpy()[:hlocs.size].view(np.uint32), hlocs)
+    assert np.array_equal(d_cnt.cpu().numpy().view(np.uint32), np.diff(hoff).astype(np.uint32))
+    d_cnt2 = torch.zeros(n, dtype=torch.int32, device=dev)
+    ix.count_batch_async(d_data.data_ptr(), d_off.data_ptr(), n, d_cnt2.data_ptr())
+    ix.sync()
+    assert torch.equal(d_cnt, d_cnt2)
+    ix.timing_enable(True)
+    ix.locate_batch_async(d_data.data_ptr(), d_off.data_ptr(), n, d_loff.data_ptr(), d_locs.data_ptr(), cap,
+                          d_need.data_ptr(), d_ws.data_ptr(), ws)
+    ix.sync()
+    t = ix.timing_read()
+    assert t["count"]["launches"] == 1 and t["locate"]["launches"] == 1 and t["count"]["total_ms"] > 0
+    ix.close()
+
+
+def test_load_device_blob(pkg, O):
+    """fmx_build_device + fmx_load_device: the blob never leaves HBM."""
+    import torch
+    rng = np.random.default_rng(5)
+    table = pkg.text_encoders.EncodingTable.from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=100_000).astype(np.uint8)
+    b = (pkg.FmIndexBuilder(text.size, 5, table, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    size = b.blob_size()
+    dev = torch.device("cuda:0")
+    d_text = torch.from_numpy(text).to(dev)
+    d_blob = torch.zeros(size, dtype=torch.uint8, device=dev)
+    b.build_device(d_text.data_ptr(), d_blob.data_ptr(), size)
+    host = d_blob.cpu().numpy()
+    ref = O.build(text.tobytes(), 5, O.layout(4, 3, 64), 3, 2, table.table)
+    assert np.array_equal(host, ref)
+    ix = pkg.FmIndex.load_device(d_blob.data_ptr(), size, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    pats = [text[s:s + 12].tobytes() for s in rng.integers(0, text.size - 12, size=500)]
+    orc = O.OracleIndex(ref, O.layout(4, 3, 64, 0))
+    data, offsets = pkg.pack_patterns(pats)
+    ooff, olocs = orc.locate_batch(data, offsets)
+    goff, glocs = ix.locate_batch((data, offsets))
+    assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    ix.close()
