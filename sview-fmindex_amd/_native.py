@@ -86,6 +86,16 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build the HIP engine first "
                 "(python -c 'import __graft_entry__ as g; g.build()')")
+        # One HIP runtime per process: when torch is installed, load its HIP
+        # runtime first (SONAME libamdhip64.so.7, as the system one), so that
+        # libfmx.so's DT_NEEDED binds to it and torch tensors / RCCL / our kernels
+        # share one device context.  Loaded the other way round, two HSA runtimes
+        # would compete for the device.
+        if os.environ.get("FMX_NO_TORCH_RUNTIME") != "1":
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)
