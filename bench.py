@@ -6,9 +6,10 @@ ACGTN (N = wildcard, sigma 5), layout u32 / Block3<u64> / EncodingTable,
 SA sampling 2, k-mer table k = 3; 100,000 x 20 bp patterns cut from the text at
 uniform random starts (bench/src/generate.rs:105-113, cold ratio 1.0), per GPU.
 
-One step = one fmx_locate_batch_async call over the batch: k-mer seed + LF loop
-(k_count), exclusive scan of the counts, sampled-SA walk (k_locate) — every
-count and every location of every pattern, written to HBM.  Inputs (text,
+One step = one fmx_locate_batch_async call over the batch = one launch of the
+fused k_locate kernel: k-mer seed + LF loop, single-pass look-back scan of the
+counts into output offsets, sampled-SA walk — every count (as offsets) and
+every location of every pattern, written to HBM.  Inputs (text,
 blob, patterns) are resident in HBM before the timed region.
 
 Multi-GPU: one process per GPU (torchrun); each rank builds its own replica of
@@ -111,7 +112,7 @@ def main():
     d_locs = torch.zeros(cap, dtype=torch.int32, device=dev)
     d_need = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = ix.locate_workspace_size(B)
-    d_ws = torch.empty(ws, dtype=torch.uint8, device=dev)
+    d_ws = torch.zeros(ws, dtype=torch.uint8, device=dev)
 
     def step():
         ix.locate_batch_async(d_pat.data_ptr(), d_off.data_ptr(), B, d_loff.data_ptr(), d_locs.data_ptr(), cap,
@@ -157,24 +158,22 @@ def main():
         gather_ms = (time.perf_counter() - tg) * 1e3
 
     # ---- roofline of the dominant kernel ------------------------------------
+    # Algorithmic bytes: per pattern m + 2P (k-mer seed) +
+    # L*2*(P+|B|) (two rank queries per LF step) + P (count), per occurrence
+    # w*(P+|B|) (walk, E[w] = sr-1) + P (sampled SA) + P (location out).
     P, BLK = 4, 24                      # u32 positions, Block3<u64> = 24 B
-    k = info["kmer_size"]
+    k, sr = info["kmer_size"], info["sampling_ratio"]
     offs_h = d_loff.cpu().numpy().view(np.uint64)
     total_occ = int(offs_h[-1])
     # every pattern is cut from the text, so its interval never empties and the
     # LF loop runs exactly m - k steps (with_slice.rs:27-31)
     L = m - k
-    count_bytes_per_pattern = m + 8 + 2 * P + L * 2 * (P + BLK) + 8 + P   # pattern, offset, seed, LF, cnt64+lo
-    locate_bytes_per_occ = 1.0 * (P + BLK) + P + P                          # E[walk]=sr-1 steps, SA, output
-    kern = {}
-    for name, t in timing.items():
-        kern[name] = t["total_ms"] / max(t["launches"], 1)
-    dominant = max(kern, key=kern.get) if kern else "count"
-    if dominant == "locate":
-        alg_bytes = locate_bytes_per_occ * total_occ + (P + 16) * B
-    else:
-        alg_bytes = count_bytes_per_pattern * B
-    achieved = alg_bytes / (kern.get(dominant, float("nan")) * 1e-3) / 1e9
+    per_pattern = m + 2 * P + L * 2 * (P + BLK) + P
+    per_occ = (sr - 1) * (P + BLK) + 2 * P
+    kern = {name: t["total_ms"] / max(t["launches"], 1) for name, t in timing.items()}
+    dominant = "locate"   # the single fused launch of a step (k_locate)
+    alg_bytes = per_pattern * B + per_occ * total_occ
+    achieved = alg_bytes / (kern[dominant] * 1e-3) / 1e9
     traffic = None
     traffic_src = None
     if os.path.exists(args.traffic_csv):
@@ -185,6 +184,16 @@ def main():
                 traffic_src = os.path.relpath(args.traffic_csv, ROOT)
         except Exception:
             pass
+
+    # size-independent property at full size: pattern i was cut at starts[i],
+    # so starts[i] must be one of its locations
+    locs_h = d_locs[:total_occ].cpu().numpy().view(np.uint32)
+    st_h = starts.cpu().numpy()
+    cnt_h = np.diff(offs_h).astype(np.int64)
+    owner = np.repeat(np.arange(B), cnt_h)
+    hit = np.zeros(B, dtype=bool)
+    hit[owner[locs_h.astype(np.int64) == st_h[owner]]] = True
+    self_found = bool(hit.all() and (cnt_h >= 1).all())
 
     value = world * B * args.steps / elapsed
     result = {
@@ -209,10 +218,12 @@ def main():
         "roofline": {
             "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-            "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": kern.get(dominant),
+            "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pattern": alg_bytes / B,
+            "avg_launch_ms": kern.get(dominant),
         },
         "kernels_ms_per_launch": kern,
         "occurrences_per_step": total_occ,
+        "self_location_check": self_found,
         "build_s": build_s,
         "gather_ms": gather_ms,
     }

@@ -1,0 +1,14 @@
+# rocprofv3 passes over the C2 bench (no CPU leg).  Kernel trace + stats in one
+# run; each PMC counter group in its own run (MI355X_MICROARCH.md, rocprofv3).
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-r1}
+ARGS=${BENCH_ARGS:-"--steps 50 --warmup 5 --no-cpu"}
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/${T}_build.log 2>&1 &&
+timeout -k 10 120 rocprofv3 -L > gpurun_out/${T}_counters.txt 2>&1;
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${T}_trace.log 2>&1 && echo trace-ok &&
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${T}_pmc1 -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${T}_pmc1.log 2>&1 && echo pmc1-ok &&
+timeout -k 10 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d gpurun_out/${T}_pmc2 -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${T}_pmc2.log 2>&1 && echo pmc2-ok &&
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY --kernel-trace -d gpurun_out/${T}_pmc3 -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${T}_pmc3.log 2>&1 && echo pmc3-ok

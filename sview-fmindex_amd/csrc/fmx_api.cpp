@@ -260,6 +260,7 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
         hipMemsetAsync(ix->d_status, 0, 4, s);
         hipStreamSynchronize(s);
     }
+    if (st & kStatusHang) return FMX_E_DEVICE;
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
     return FMX_OK;
@@ -365,6 +366,7 @@ void fmx_free(fmx_index *ix) {
         for (auto &p : t.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     for (auto e : ix->event_pool) hipEventDestroy(e);
     if (ix->d_scratch) hipFree(ix->d_scratch);
+    if (ix->d_ws) hipFree(ix->d_ws);
     if (ix->d_occ) hipFree(ix->d_occ);
     if (ix->d_status) hipFree(ix->d_status);
     if (ix->d_blob_owned) hipFree(ix->d_blob_owned);
@@ -401,53 +403,37 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
     if (!ix || (n && (!d_bytes || !d_offsets || !d_counts))) return FMX_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
     return dev_err(timed(ix, "count", s, n, [&] {
-        return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, nullptr, nullptr, s);
+        return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, s);
     }));
 }
 
-static uint64_t ws_layout(const fmx_index *ix, uint64_t n, uint64_t *o_cnt, uint64_t *o_lo, uint64_t *o_tmp,
-                          size_t *tmp_bytes) {
-    size_t tb = 0;
-    scan_workspace_bytes(n, &tb);
-    *tmp_bytes = tb;
-    *o_cnt = 0;
-    *o_lo = align_up((n + 1) * 8, 256);
-    *o_tmp = *o_lo + align_up(std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes, 256);
-    return *o_tmp + align_up(tb, 256);
-}
+// Locate workspace: [ctl: 2 x u32, padded to 256 B][tiles: 2 x tiles_cap x u64].
+static uint64_t ws_bytes_for(uint64_t n) { return 256 + 2 * locate_tiles_cap(n) * 8; }
 
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {
     if (!ix || !bytes) return FMX_E_ARG;
-    uint64_t a, b, c;
-    size_t t;
-    *bytes = ws_layout(ix, n, &a, &b, &c, &t);
+    *bytes = ws_bytes_for(n);
     return FMX_OK;
 }
 
 fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                   uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs,
                                   uint64_t cap, uint64_t *d_needed, void *d_ws, uint64_t ws_bytes, void *stream) {
-    if (!ix || !d_loc_offsets || (n && (!d_bytes || !d_offsets)) || (cap && !d_locs)) return FMX_E_ARG;
+    if (!ix || !d_loc_offsets || !d_needed || (n && (!d_bytes || !d_offsets)) || (cap && !d_locs)) return FMX_E_ARG;
+    if (!d_ws || ws_bytes < 256 + 16) return FMX_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
-    uint64_t o_cnt, o_lo, o_tmp;
-    size_t tb;
-    const uint64_t need = ws_layout(ix, n, &o_cnt, &o_lo, &o_tmp, &tb);
-    if (!d_ws || ws_bytes < need) return FMX_E_ARG;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_loc_offsets, 0, 8, s);
+        if (e == hipSuccess) e = hipMemsetAsync(d_needed, 0, 8, s);
+        return dev_err(e);
+    }
+    const uint64_t tiles_cap = (ws_bytes - 256) / 16;
+    if (tiles_cap < locate_tiles_cap(n)) return FMX_E_ARG;
     uint8_t *ws = (uint8_t *)d_ws;
-    uint64_t *cnt64 = (uint64_t *)(ws + o_cnt);
-    void *lo = ws + o_lo;
-    hipError_t e = hipMemsetAsync(cnt64 + n, 0, 8, s);
-    if (e == hipSuccess)
-        e = timed(ix, "count", s, n, [&] {
-            return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, cnt64, lo, s);
-        });
-    if (e == hipSuccess)
-        e = timed(ix, "scan", s, n, [&] { return launch_scan(cnt64, d_loc_offsets, n + 1, ws + o_tmp, tb, s); });
-    if (e == hipSuccess && d_needed)
-        e = hipMemcpyAsync(d_needed, d_loc_offsets + n, 8, hipMemcpyDeviceToDevice, s);
-    if (e == hipSuccess)
-        e = timed(ix, "locate", s, n, [&] { return launch_locate(ix, d_loc_offsets, lo, n, d_locs, cap, s); });
-    return dev_err(e);
+    return dev_err(timed(ix, "locate", s, n, [&] {
+        return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
+                             (uint32_t *)ws, (uint64_t *)(ws + 256), tiles_cap, s);
+    }));
 }
 
 fmx_status fmx_sync(fmx_index *ix, void *stream) {
@@ -489,6 +475,20 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     return read_status(ix, s);
 }
 
+// The host-API locate workspace lives in the index, zeroed when (re)allocated.
+static fmx_status ensure_ws(fmx_index *ix, uint64_t n) {
+    const uint64_t need = ws_bytes_for(n);
+    if (ix->ws_bytes >= need) return FMX_OK;
+    if (ix->d_ws) hipFree(ix->d_ws);
+    ix->d_ws = nullptr;
+    ix->ws_bytes = 0;
+    const uint64_t want = std::max<uint64_t>(need, 1 << 16);
+    if (hipMalloc(&ix->d_ws, want) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMemset(ix->d_ws, 0, want) != hipSuccess) return FMX_E_DEVICE;
+    ix->ws_bytes = want;
+    return FMX_OK;
+}
+
 fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets, uint64_t n,
                             uint32_t flags, uint64_t *out_loc_offsets, void *out_locs, uint64_t cap,
                             uint64_t *needed) {
@@ -500,58 +500,48 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
     if (st) return st;
     hipSetDevice(ix->device);
     const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
-    uint64_t o_cnt, o_lo, o_tmp;
-    size_t tb;
-    const uint64_t wsb = ws_layout(ix, n, &o_cnt, &o_lo, &o_tmp, &tb);
+    st = ensure_ws(ix, n);
+    if (st) return st;
     const uint64_t o_off = align_up(nb, 256);
     const uint64_t o_loff = o_off + align_up((n + 1) * 8, 256);
-    const uint64_t o_ws = o_loff + align_up((n + 1) * 8, 256);
-    const uint64_t o_locs = o_ws + align_up(wsb, 256);
-    st = ensure_scratch(ix, o_locs);
-    if (st) return st;
+    const uint64_t o_need = o_loff + align_up((n + 1) * 8, 256);
+    const uint64_t o_locs = o_need + 256;
     hipStream_t s = ix->stream;
-    uint8_t *d = ix->d_scratch;
-    hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
-    // phase 1: SA intervals and their exclusive scan
-    uint8_t *ws = d + o_ws;
-    uint64_t *cnt64 = (uint64_t *)(ws + o_cnt);
-    uint64_t *loff = (uint64_t *)(d + o_loff);
-    if (e == hipSuccess) e = hipMemsetAsync(cnt64 + n, 0, 8, s);
-    if (e == hipSuccess)
-        e = timed(ix, "count", s, n, [&] {
-            return launch_count(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, cnt64, ws + o_lo, s);
-        });
-    if (e == hipSuccess)
-        e = timed(ix, "scan", s, n, [&] { return launch_scan(cnt64, loff, n + 1, ws + o_tmp, tb, s); });
-    if (e == hipSuccess) e = hipMemcpyAsync(out_loc_offsets, loff, (n + 1) * 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return FMX_E_DEVICE;
-    st = read_status(ix, s);
-    if (st) return st;
-    const uint64_t total = out_loc_offsets[n];
-    if (needed) *needed = total;
-    if (total > cap) return FMX_E_CAPACITY;
-    // phase 2: the walk, into scratch sized for exactly `total` locations
-    st = ensure_scratch(ix, o_locs + std::max<uint64_t>(total, 1) * pb);
-    if (st) return st;
-    if (ix->d_scratch != d) {  // scratch moved: re-upload what phase 2 reads
-        d = ix->d_scratch;
-        ws = d + o_ws;
-        loff = (uint64_t *)(d + o_loff);
-        // lo[] lived in the old scratch: recompute phase 1 into the new one
-        cnt64 = (uint64_t *)(ws + o_cnt);
-        e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
+    // Guess the output size (one occurrence per pattern, or what scratch
+    // already holds); if the patterns have more occurrences, grow and rerun.
+    uint64_t dcap = std::min<uint64_t>(cap, std::max<uint64_t>(n, ix->scratch_bytes > o_locs
+                                                                       ? (ix->scratch_bytes - o_locs) / pb : 0));
+    for (int pass = 0; pass < 2; ++pass) {
+        st = ensure_scratch(ix, o_locs + std::max<uint64_t>(dcap, 1) * pb);
+        if (st) return st;
+        uint8_t *d = ix->d_scratch;
+        hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = launch_count(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, cnt64, ws + o_lo, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(loff, out_loc_offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return FMX_E_DEVICE;
+        st = fmx_locate_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, (uint64_t *)(d + o_loff),
+                                    d + o_locs, dcap, (uint64_t *)(d + o_need), ix->d_ws, ix->ws_bytes, s);
+        if (st) return st;
+        uint64_t total = 0;
+        e = hipMemcpyAsync(&total, d + o_need, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return FMX_E_DEVICE;
+        st = read_status(ix, s);
+        if (st) return st;
+        if (needed) *needed = total;
+        if (total > cap) {
+            if (hipMemcpy(out_loc_offsets, d + o_loff, (n + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+                return FMX_E_DEVICE;
+            return FMX_E_CAPACITY;
+        }
+        if (total <= dcap) {
+            e = hipMemcpyAsync(out_loc_offsets, d + o_loff, (n + 1) * 8, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess && total) e = hipMemcpyAsync(out_locs, d + o_locs, total * pb, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            return dev_err(e);
+        }
+        dcap = total;  // second pass with room for every location
     }
-    e = timed(ix, "locate", s, n, [&] { return launch_locate(ix, loff, ws + o_lo, n, d + o_locs, total, s); });
-    if (e == hipSuccess && total) e = hipMemcpyAsync(out_locs, d + o_locs, total * pb, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return FMX_E_DEVICE;
-    return read_status(ix, s);
+    return FMX_E_DEVICE;
 }
 
 // ---------------------------------------------------------------- timing

@@ -66,6 +66,7 @@ struct QueryArgs {
 // Device status bits
 constexpr uint32_t kStatusEmpty = 1u;
 constexpr uint32_t kStatusSymbol = 2u;
+constexpr uint32_t kStatusHang = 4u;  // a bounded look-back spin gave up
 
 struct Timer {
     std::string name;
@@ -92,9 +93,11 @@ struct fmx_index {
     uint32_t rec_bytes = 0;
     uint32_t *d_status = nullptr;
     fmx::QueryArgs qa{};
-    // host-API scratch (grown on demand)
+    // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
+    uint8_t *d_ws = nullptr;
+    uint64_t ws_bytes = 0;
     // timing
     bool timing = false;
     std::vector<fmx::Timer> timers;
@@ -105,14 +108,16 @@ struct fmx_index {
 namespace fmx {
 
 // Query launchers (fmx_query.hip).  All asynchronous on `stream`.
-hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
-                        uint64_t n, uint32_t flags, void *d_counts_p, uint64_t *d_counts_u64,
-                        void *d_lo_p, hipStream_t stream);
-hipError_t launch_locate(const fmx_index *ix, const uint64_t *d_loc_offsets, const void *d_lo_p,
-                         uint64_t n, void *d_locs, uint64_t cap, hipStream_t stream);
-hipError_t scan_workspace_bytes(uint64_t n, size_t *bytes);
-hipError_t launch_scan(const uint64_t *d_in, uint64_t *d_out, uint64_t n_plus_1, void *tmp,
-                       size_t tmp_bytes, hipStream_t stream);
+hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                        uint32_t flags, void *d_counts, hipStream_t stream);
+// Fused count + offsets scan + locate.  d_ctl (2 x u32) and d_tiles
+// (2 x tiles_cap x u64) must be zero before their first use; the kernel keeps
+// them consistent across launches on one stream.
+hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                         uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
+                         uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
+                         hipStream_t stream);
+uint64_t locate_tiles_cap(uint64_t n);
 hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
 uint32_t interleaved_record_bytes(const BlobView &bv);
 

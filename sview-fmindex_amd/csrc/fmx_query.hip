@@ -1,17 +1,19 @@
 // fmx_query.hip — gfx950 kernels for the FM-index query hot path.
 //
-//   k_count    : k-mer seed + backward-search LF loop, one lane per pattern
-//                (FmIndex::get_pos_range, src/locate/with_slice.rs:21-33;
-//                 next_pos_range, src/locate/mod.rs:38-45;
-//                 BwmView::get_next_rank, components/bwm/mod.rs:197-215;
-//                 CountArrayView seed, components/count_array.rs:203-233)
-//   k_locate   : sampled-SA locate walk, one lane per occurrence row, rows
-//                balanced across the 64 lanes of a wavefront
-//                (write_locations_to_buffer, src/locate/mod.rs:14-37;
-//                 get_pre_rank_and_symidx, components/bwm/mod.rs:217-236;
-//                 SuffixArrayView::get_location_of, suffix_array/mod.rs:100-105)
-//   k_relayout : optional one-time re-layout of (rank checkpoint, bit planes)
-//                into one HBM record per block (FMX_OCC_INTERLEAVED).
+//   k_count   : k-mer seed + backward-search LF loop, one lane per pattern
+//               (FmIndex::get_pos_range, src/locate/with_slice.rs:21-33;
+//                next_pos_range, src/locate/mod.rs:38-45;
+//                BwmView::get_next_rank, components/bwm/mod.rs:197-215;
+//                CountArrayView seed, components/count_array.rs:203-233)
+//   k_locate  : one launch for a whole count+locate batch: the k_count body,
+//               then a single-pass decoupled look-back scan of the counts
+//               (output offsets), then the sampled-SA locate walk of every
+//               occurrence row, rows dealt across the 64 lanes of a wavefront
+//               (write_locations_to_buffer, src/locate/mod.rs:14-37;
+//                get_pre_rank_and_symidx, components/bwm/mod.rs:217-236;
+//                SuffixArrayView::get_location_of, suffix_array/mod.rs:100-105)
+//   k_relayout: optional one-time re-layout of (rank checkpoints, bit planes)
+//               into one HBM record per block (FMX_OCC_INTERLEAVED).
 //
 // All integer work: no MFMA.  The hot loop is a chain of dependent random
 // gathers, so the kernels keep many independent chains (lanes) in flight and
@@ -37,7 +39,8 @@ template <int N, int VB>
 struct Planes {
     using W = typename VecT<VB>::W;
     static constexpr int WPP = VecT<VB>::WPP;
-    W w[N * WPP];
+    static constexpr int WORDS = N * WPP;
+    W w[WORDS];
 
     // Block::get_remain_count_of (block3.rs:42-55): occurrences of symbol c among
     // the first `rem` symbols of the block (MSB-first); rem == 0 gives 0.
@@ -77,190 +80,162 @@ struct Planes {
         }
         return s;
     }
+
+    __device__ __forceinline__ void load(const uint8_t *p) {
+        const W *src = reinterpret_cast<const W *>(p);
+#pragma unroll
+        for (int j = 0; j < WORDS; ++j) w[j] = src[j];
+    }
 };
+
+// Select v[idx] (idx < K) with a tree of v_cndmask on the bits of idx: a
+// compare-against-constant chain gets lowered to a scratch-memory table
+// lookup by the compiler, this form stays in registers.
+template <int K, typename T>
+__device__ __forceinline__ T tree_pick(const T *v, uint32_t idx) {
+    if constexpr (K == 1) {
+        return v[0];
+    } else {
+        const T lo = tree_pick<K / 2>(v, idx);
+        const T hi = tree_pick<K / 2>(v + K / 2, idx);
+        return (idx & (K / 2)) ? hi : lo;
+    }
+}
+
+constexpr int pow2_ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
 // ------------------------------------------------------- occ access (rank)
 
-// Blob layout: rank_checkpoints and blocks are separate arrays
-// (bwm/mod.rs:145-190).  REC == 0.
-// Interleaved layout: record q = [planes (N*VB/8 B)][ckpt[0..sigma) (P each)][pad]
-// of REC bytes (64 or 128), one HBM line per LF step.
+// REC == 0 — blob layout: rank_checkpoints [P; blocks*sigma] and blocks
+//            [BlockN<V>; blocks] are separate arrays (bwm/mod.rs:145-190).
+// REC > 0  — interleaved layout: record q (REC = 64 or 128 bytes, aligned) is
+//            [ckpt[0..sigma) as P][pad][bit planes at REC - N*VB/8], so one
+//            LF step reads one HBM line.
 template <typename P, int N, int VB, int REC>
 struct Occ {
     static constexpr int PLANE_BYTES = N * VB / 8;
-    static constexpr int MAXC = REC == 0 ? 1 : (REC - PLANE_BYTES) / (int)sizeof(P);
-
-    // A fetched block: planes + (blob mode) the one checkpoint asked for, or
-    // (interleaved) every checkpoint of the record.
-    struct Rec {
-        Planes<N, VB> pl;
-        P ck[MAXC];
-    };
-
-    __device__ __forceinline__ static void fetch_planes(const QueryArgs &a, uint64_t q, Planes<N, VB> &pl) {
-        using W = typename VecT<VB>::W;
-        const W *bp = reinterpret_cast<const W *>(a.blocks) + q * (uint64_t)(N * VecT<VB>::WPP);
-#pragma unroll
-        for (int j = 0; j < N * VecT<VB>::WPP; ++j) pl.w[j] = bp[j];
-    }
-
-    // Interleaved: load the whole record with 16-byte loads.
-    __device__ __forceinline__ static void fetch_record(const QueryArgs &a, uint64_t q, Rec &r) {
-        static_assert(REC == 64 || REC == 128, "record size");
-        const uint4 *rp = reinterpret_cast<const uint4 *>(a.occ + q * (uint64_t)REC);
-        uint32_t words[REC / 4];
-#pragma unroll
-        for (int i = 0; i < REC / 16; ++i) {
-            const uint4 v = rp[i];
-            words[4 * i + 0] = v.x; words[4 * i + 1] = v.y; words[4 * i + 2] = v.z; words[4 * i + 3] = v.w;
-        }
-        using W = typename VecT<VB>::W;
-#pragma unroll
-        for (int j = 0; j < N * VecT<VB>::WPP; ++j) {
-            if constexpr (sizeof(W) == 8) r.pl.w[j] = (uint64_t)words[2 * j] | ((uint64_t)words[2 * j + 1] << 32);
-            else r.pl.w[j] = words[j];
-        }
-#pragma unroll
-        for (int i = 0; i < MAXC; ++i) {
-            constexpr int base = PLANE_BYTES / 4;
-            if constexpr (sizeof(P) == 8) r.ck[i] = (P)((uint64_t)words[base + 2 * i] | ((uint64_t)words[base + 2 * i + 1] << 32));
-            else r.ck[i] = (P)words[base + i];
-        }
-    }
-
-    __device__ __forceinline__ static P pick(const Rec &r, uint32_t c) {
-        P v = r.ck[0];
-#pragma unroll
-        for (int i = 1; i < MAXC; ++i) v = (c == (uint32_t)i) ? r.ck[i] : v;
-        return v;
-    }
+    static constexpr int PLANE_OFF = REC - PLANE_BYTES;
+    static constexpr int NCK = REC == 0 ? (1 << N) : PLANE_OFF / (int)sizeof(P);  // checkpoint slots
+    static constexpr int NCK2 = pow2_ceil(NCK);
 
     // Occ(c, stored position p): BwmView::get_next_rank after the sentinel
-    // adjustment (bwm/mod.rs:206-214).
+    // adjustment (bwm/mod.rs:206-214).  c is known before the loads, so only
+    // the planes and the one checkpoint are fetched, all independently.
     __device__ __forceinline__ static P rank_at(const QueryArgs &a, P p, uint32_t c) {
         const uint64_t q = (uint64_t)p / VB;
         const uint32_t rem = (uint32_t)((uint64_t)p % VB);
+        Planes<N, VB> pl;
+        P ck;
         if constexpr (REC == 0) {
-            const P ck = reinterpret_cast<const P *>(a.ckpt)[q * a.sigma + c];
-            Planes<N, VB> pl;
-            fetch_planes(a, q, pl);
-            return ck + (P)pl.rank(rem, c);
+            ck = reinterpret_cast<const P *>(a.ckpt)[q * a.sigma + c];
+            pl.load(a.blocks + q * PLANE_BYTES);
         } else {
-            Rec r;
-            fetch_record(a, q, r);
-            return pick(r, c) + (P)r.pl.rank(rem, c);
+            const uint8_t *r = a.occ + q * REC;
+            ck = reinterpret_cast<const P *>(r)[c];
+            pl.load(r + PLANE_OFF);
         }
+        return ck + (P)pl.rank(rem, c);
     }
 
-    // get_pre_rank_and_symidx body (bwm/mod.rs:223-235) for stored position p.
+    // get_pre_rank_and_symidx body (bwm/mod.rs:223-235) for stored position p:
+    // the symbol is only known after the planes arrive, so every checkpoint
+    // slot of the block is fetched alongside them (one round trip) and the
+    // right one selected in registers.
     __device__ __forceinline__ static P pre_rank_sym(const QueryArgs &a, P p, uint32_t &c) {
         const uint64_t q = (uint64_t)p / VB;
         const uint32_t rem = (uint32_t)((uint64_t)p % VB);
+        Planes<N, VB> pl;
         if constexpr (REC == 0) {
-            Planes<N, VB> pl;
-            fetch_planes(a, q, pl);
+            pl.load(a.blocks + q * PLANE_BYTES);
             const P *ckq = reinterpret_cast<const P *>(a.ckpt) + q * a.sigma;
             if constexpr (N <= 3) {
-                // sigma <= 8: fetch every checkpoint of the block alongside the
-                // planes so the step costs one round trip, not two.
-                P all[1 << N];
+                P all[NCK2];
 #pragma unroll
-                for (int i = 0; i < (1 << N); ++i) all[i] = (uint32_t)i < a.sigma ? ckq[i] : P(0);
+                for (int i = 0; i < NCK2; ++i) all[i] = (uint32_t)i < a.sigma ? ckq[i] : P(0);
                 c = pl.sym(rem);
-                P ck = all[0];
-#pragma unroll
-                for (int i = 1; i < (1 << N); ++i) ck = (c == (uint32_t)i) ? all[i] : ck;
-                return ck + (P)pl.rank(rem, c);
+                return tree_pick<NCK2>(all, c) + (P)pl.rank(rem, c);
             } else {
                 c = pl.sym(rem);
                 return ckq[c] + (P)pl.rank(rem, c);
             }
         } else {
-            Rec r;
-            fetch_record(a, q, r);
-            c = r.pl.sym(rem);
-            return pick(r, c) + (P)r.pl.rank(rem, c);
+            const uint8_t *r = a.occ + q * REC;
+            P all[NCK2];
+            const P *ckr = reinterpret_cast<const P *>(r);
+#pragma unroll
+            for (int i = 0; i < NCK2; ++i) all[i] = i < NCK ? ckr[i] : P(0);
+            pl.load(r + PLANE_OFF);
+            c = pl.sym(rem);
+            return tree_pick<NCK2>(all, c) + (P)pl.rank(rem, c);
         }
     }
 };
 
-// ----------------------------------------------------------------- k_count
+// ----------------------------------------------------- shared kernel parts
 
-template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
-                                               const uint64_t *__restrict__ offs, uint64_t npat,
-                                               uint32_t flags, P *__restrict__ out_cnt,
-                                               uint64_t *__restrict__ cnt64, P *__restrict__ out_lo) {
-    using O = Occ<P, N, VB, REC>;
-    __shared__ uint8_t s_enc[256];
-    __shared__ P s_C[kMaxSigma + 1];
-    __shared__ uint64_t s_mult[kMaxK];
+template <typename P>
+struct Tables {
+    uint8_t enc[256];
+    P C[kMaxSigma + 1];
+    uint64_t mult[kMaxK];
+};
+
+template <typename P>
+__device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s) {
     const int t = threadIdx.x;
-    s_enc[t] = a.enc[t];
-    if ((uint32_t)t <= a.sigma) s_C[t] = (P)a.C[t];
-    if ((uint32_t)t < a.k) s_mult[t] = a.mult[t];
-    __syncthreads();
-
-    const uint64_t i = (uint64_t)blockIdx.x * 256u + t;
-    if (i >= npat) return;
-    const uint64_t beg = offs[i];
-    const uint64_t m = offs[i + 1] - beg;
-    const uint8_t *p = bytes + beg;
-    const bool rev = flags & FMX_PATTERN_REVERSED;
-    const uint32_t sigma = a.sigma, k = a.k;
-    const P sent = (P)a.sentinel;
-    uint32_t bad = 0;
-    P lo = 0, hi = 0;
-
-    if (m == 0) {
-        bad = kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
-    } else {
-        // k-mer seed: count_array.rs:203-233.  Pattern position j is p[j]
-        // (forward) or p[m-1-j] (bytes given reversed, with_rev_iter.rs).
-        uint64_t s = 0, e, idx;
-        const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
-        for (uint64_t j = 0; j < take; ++j) {
-            const uint64_t pj = first + j;
-            const uint8_t b = p[rev ? m - 1 - pj : pj];
-            const uint32_t c = s_enc[b];
-            if (c >= sigma) bad = kStatusSymbol;
-            s += (uint64_t)(c + 1) * s_mult[j];
-        }
-        if (m < k) { e = s + s_mult[m - 1] - 1; idx = 0; }
-        else { e = s; idx = m - k; }
-        const P *kt = reinterpret_cast<const P *>(a.kmer);
-        if (!bad) { lo = kt[s - 1]; hi = kt[e]; }
-        // LF loop: with_slice.rs:27-31 / next_pos_range (locate/mod.rs:39-45)
-        while (!bad && lo < hi && idx > 0) {
-            idx -= 1;
-            const uint8_t b = p[rev ? m - 1 - idx : idx];
-            const uint32_t c = s_enc[b];
-            if (c >= sigma) { bad = kStatusSymbol; break; }
-            const P pre = s_C[c];
-            const P plo = lo + (lo < sent ? P(1) : P(0));  // bwm/mod.rs:202-204
-            const P phi = hi + (hi < sent ? P(1) : P(0));
-            const P rlo = O::rank_at(a, plo, c);
-            const P rhi = O::rank_at(a, phi, c);
-            lo = pre + rlo;
-            hi = pre + rhi;
-        }
-    }
-    if (bad) {
-        atomicOr(a.status, bad);
-        lo = hi = 0;
-    }
-    const P cnt = hi - lo;
-    if (out_cnt) out_cnt[i] = cnt;
-    if (cnt64) cnt64[i] = (uint64_t)cnt;
-    if (out_lo) out_lo[i] = lo;
+    s.enc[t] = a.enc[t];
+    if ((uint32_t)t <= a.sigma) s.C[t] = (P)a.C[t];
+    if ((uint32_t)t < a.k) s.mult[t] = a.mult[t];
 }
 
-// ---------------------------------------------------------------- k_locate
+// k-mer seed + LF loop for pattern bytes p[0..m): FmIndex::get_pos_range
+// (with_slice.rs:21-33).  Pattern position j is p[j], or p[m-1-j] when the
+// bytes were given reversed (the *_rev_iter forms, with_rev_iter.rs).
+// Returns status bits (0 = ok).
+template <typename P, int N, int VB, int REC>
+__device__ __forceinline__ uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p, uint64_t m,
+                                           bool rev, P &lo, P &hi) {
+    using O = Occ<P, N, VB, REC>;
+    const uint32_t sigma = a.sigma, k = a.k;
+    const P sent = (P)a.sentinel;
+    lo = hi = 0;
+    if (m == 0) return kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
+    // seed: count_array.rs:203-233
+    uint64_t code = 0, e, idx;
+    const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
+    uint32_t bad = 0;
+    for (uint64_t j = 0; j < take; ++j) {
+        const uint64_t pj = first + j;
+        const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+        bad |= c >= sigma;
+        code += (uint64_t)(c + 1) * s.mult[j];
+    }
+    if (bad) return kStatusSymbol;
+    if (m < k) { e = code + s.mult[m - 1] - 1; idx = 0; }
+    else { e = code; idx = m - k; }
+    const P *kt = reinterpret_cast<const P *>(a.kmer);
+    lo = kt[code - 1];
+    hi = kt[e];
+    // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
+    while (lo < hi && idx > 0) {
+        idx -= 1;
+        const uint32_t c = s.enc[p[rev ? m - 1 - idx : idx]];
+        if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
+        const P plo = lo + (lo < sent ? P(1) : P(0));  // bwm/mod.rs:202-204
+        const P phi = hi + (hi < sent ? P(1) : P(0));
+        const P rlo = O::rank_at(a, plo, c);
+        const P rhi = O::rank_at(a, phi, c);
+        const P pre = s.C[c];
+        lo = pre + rlo;
+        hi = pre + rhi;
+    }
+    return 0;
+}
 
 // Walk one suffix-array row to a sampled row or to the text start
 // (locate/mod.rs:19-35; suffix_array/mod.rs:100-105).
 template <typename P, int N, int VB, int REC>
-__device__ __forceinline__ P walk_row(const QueryArgs &a, const P *s_C, P pos) {
+__device__ __forceinline__ P walk_row(const QueryArgs &a, const P *C, P pos) {
     using O = Occ<P, N, VB, REC>;
     const P sent = (P)a.sentinel;
     const P sr = (P)a.sr;
@@ -271,46 +246,173 @@ __device__ __forceinline__ P walk_row(const QueryArgs &a, const P *s_C, P pos) {
         const P p = pos + (pos < sent ? P(1) : P(0));
         uint32_t c;
         const P rank = O::pre_rank_sym(a, p, c);
-        pos = s_C[c] + rank;
+        pos = C[c] + rank;
         off += 1;
     }
     const P *sa = reinterpret_cast<const P *>(a.sa);
-    return sa[mask ? (uint64_t)pos >> (__builtin_popcount(a.sr_pow2_mask)) : (uint64_t)(pos / sr)] + off;
+    const uint64_t slot = mask ? (uint64_t)pos >> __builtin_popcount(a.sr_pow2_mask) : (uint64_t)(pos / sr);
+    return sa[slot] + off;
 }
 
-// Rows of the wave's 64 patterns are dealt to its 64 lanes in turns of 64
-// consecutive output slots: a pattern with many occurrences is spread over
-// all lanes instead of serialising one lane.
-template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint64_t *__restrict__ loc_off,
-                                                const P *__restrict__ lo_arr, uint64_t npat,
-                                                P *__restrict__ out, uint64_t cap) {
-    __shared__ P s_C[kMaxSigma + 1];
-    if ((uint32_t)threadIdx.x <= a.sigma) s_C[threadIdx.x] = (P)a.C[threadIdx.x];
+// 256-thread workgroup exclusive scan of one u64 per thread.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total, uint64_t *sh /*[4]*/) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
     __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < w) before += sh[i];
+        all += sh[i];
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
+}
+
+// ----------------------------------------------------------------- k_count
+
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
+                                               const uint64_t *__restrict__ offs, uint64_t npat,
+                                               uint32_t flags, P *__restrict__ out_cnt) {
+    __shared__ Tables<P> s;
+    stage_tables(a, s);
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= npat) return;
+    const uint64_t beg = offs[i];
+    P lo, hi;
+    const uint32_t bad = search<P, N, VB, REC>(a, s, bytes + beg, offs[i + 1] - beg,
+                                               (flags & FMX_PATTERN_REVERSED) != 0, lo, hi);
+    if (bad) atomicOr(a.status, bad);
+    out_cnt[i] = hi - lo;
+}
+
+// ---------------------------------------------------------------- k_locate
+
+// Look-back tile word: (inclusive-or-aggregate sum << 2) | flag.
+constexpr uint64_t kTileAgg = 1, kTileInc = 2;
+
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t *__restrict__ bytes,
+                                                const uint64_t *__restrict__ offs, uint64_t npat, uint32_t flags,
+                                                P *__restrict__ out_cnt, uint64_t *__restrict__ loc_off,
+                                                P *__restrict__ out_locs, uint64_t cap, uint64_t *__restrict__ needed,
+                                                uint32_t *__restrict__ ctl, uint64_t *__restrict__ tiles,
+                                                uint32_t tiles_cap) {
+    __shared__ Tables<P> s;
+    __shared__ uint64_t s_scan[4];
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_tile, s_par;
+    stage_tables(a, s);
+    const uint32_t G = (uint32_t)((npat + 255) / 256);
+    if (threadIdx.x == 0) {
+        // Dynamic tile id: tiles are numbered in the order workgroups start, so
+        // a look-back only ever waits on workgroups that are already running.
+        const uint32_t par = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t g = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == G - 1) {  // last id handed out: reset for the next launch
+            __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[1], par ^ 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_tile = g;
+        s_par = par;
+    }
+    __syncthreads();
+    const uint32_t g = s_tile;
+    uint64_t *cur = tiles + (uint64_t)s_par * tiles_cap;
+    uint64_t *nxt = tiles + (uint64_t)(s_par ^ 1u) * tiles_cap;
+    // clear the other tile buffer for the next launch (this launch never reads it)
+    for (uint64_t x = (uint64_t)g * 256 + threadIdx.x; x < tiles_cap; x += (uint64_t)G * 256) nxt[x] = 0;
+
+    // ---- 1. SA interval of every pattern of the tile ----------------------
+    const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
+    P lo = 0, hi = 0;
+    if (i < npat) {
+        const uint64_t beg = offs[i];
+        const uint32_t bad = search<P, N, VB, REC>(a, s, bytes + beg, offs[i + 1] - beg,
+                                                   (flags & FMX_PATTERN_REVERSED) != 0, lo, hi);
+        if (bad) atomicOr(a.status, bad);
+        if (out_cnt) out_cnt[i] = hi - lo;
+    }
+    const uint64_t cnt = (uint64_t)(hi - lo);
+
+    // ---- 2. output offsets: single-pass scan with decoupled look-back -----
+    uint64_t agg;
+    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        if (g == 0) {
+            if (lane == 0) {
+                __hip_atomic_store(&cur[0], (agg << 2) | kTileInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_prefix = 0;
+            }
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&cur[g], (agg << 2) | kTileAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t prefix = 0;
+            int64_t j = (int64_t)g - 1;
+            uint32_t spins = 0;
+            while (true) {
+                const int64_t idx = j - lane;
+                const uint64_t w = idx >= 0
+                    ? __hip_atomic_load(&cur[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : kTileInc;  // before tile 0: an inclusive prefix of 0
+                const uint64_t incm = __ballot((w & 3) == kTileInc);
+                const uint64_t zerom = __ballot((w & 3) == 0);
+                const int first_inc = incm ? __builtin_ctzll(incm) : 64;
+                const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
+                if (zerom & upto) {  // a predecessor has not published yet
+                    if (++spins > (1u << 24)) { atomicOr(a.status, kStatusHang); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint64_t v = lane <= first_inc ? (w >> 2) : 0;
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
+                prefix += v;
+                if (first_inc < 64) break;
+                j -= 64;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(&cur[g], ((prefix + agg) << 2) | kTileInc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                s_prefix = prefix;
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t my_off = s_prefix + excl;
+    if (i < npat) loc_off[i] = my_off;
+    if (g == G - 1 && threadIdx.x == 0) {
+        loc_off[npat] = s_prefix + agg;
+        *needed = s_prefix + agg;
+    }
+
+    // ---- 3. locate walk, rows of the wave's 64 patterns dealt to its lanes --
     const int lane = threadIdx.x & 63;
-    const uint64_t base = ((uint64_t)blockIdx.x * 256u + threadIdx.x - lane);
-    if (base >= npat) return;  // wave-uniform
-    const uint64_t idx = base + lane;
-    const uint64_t my_off = loc_off[idx < npat ? idx : npat];
-    const P my_lo = idx < npat ? lo_arr[idx] : P(0);
     const uint64_t start = __shfl(my_off, 0);
-    const uint64_t end = loc_off[base + 64 < npat ? base + 64 : npat];
+    const uint64_t end = __shfl(my_off + cnt, 63);
     for (uint64_t t0 = start; t0 < end; t0 += 64) {
         const uint64_t t = t0 + lane;
-        // largest j with off[j] <= t (off[0] = start <= t)
-        int j = 0;
+        int jl = 0;  // largest lane whose first slot is <= t
 #pragma unroll
         for (int step = 32; step > 0; step >>= 1) {
-            const uint64_t o = __shfl(my_off, j + step);
-            if (o <= t) j += step;
+            const uint64_t o = __shfl(my_off, jl + step);
+            if (o <= t) jl += step;
         }
-        const P lo_j = __shfl(my_lo, j);
-        const uint64_t off_j = __shfl(my_off, j);
+        const P lo_j = __shfl(lo, jl);
+        const uint64_t off_j = __shfl(my_off, jl);
         if (t < end) {
-            const P row = lo_j + (P)(t - off_j);
-            const P loc = walk_row<P, N, VB, REC>(a, s_C, row);
-            if (t < cap) out[t] = loc;
+            const P loc = walk_row<P, N, VB, REC>(a, s.C, lo_j + (P)(t - off_j));
+            if (t < cap) out_locs[t] = loc;
         }
     }
 }
@@ -319,20 +421,20 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint64_
 
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_relayout(const QueryArgs a, uint64_t blocks_len, uint8_t *__restrict__ occ) {
-    constexpr int PB = N * VB / 8;
+    constexpr int PB = N * VB / 8, POFF = REC - PB;
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= blocks_len) return;
     uint32_t words[REC / 4];
 #pragma unroll
     for (int i = 0; i < REC / 4; ++i) words[i] = 0;
-    const uint32_t *bp = reinterpret_cast<const uint32_t *>(a.blocks + q * PB);
-#pragma unroll
-    for (int i = 0; i < PB / 4; ++i) words[i] = bp[i];
     const uint32_t *cp = reinterpret_cast<const uint32_t *>(a.ckpt + q * a.sigma * sizeof(P));
     const uint32_t cw = a.sigma * (uint32_t)(sizeof(P) / 4);
 #pragma unroll
-    for (int i = 0; i < (REC - PB) / 4; ++i)
-        if ((uint32_t)i < cw) words[PB / 4 + i] = cp[i];
+    for (int i = 0; i < POFF / 4; ++i)
+        if ((uint32_t)i < cw) words[i] = cp[i];
+    const uint32_t *bp = reinterpret_cast<const uint32_t *>(a.blocks + q * PB);
+#pragma unroll
+    for (int i = 0; i < PB / 4; ++i) words[POFF / 4 + i] = bp[i];
     uint4 *rp = reinterpret_cast<uint4 *>(occ + q * REC);
 #pragma unroll
     for (int i = 0; i < REC / 16; ++i)
@@ -392,23 +494,29 @@ static hipError_t dispatch(const fmx_index *ix, F &&f) {
 
 static inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
 
-hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
-                        uint64_t n, uint32_t flags, void *d_counts_p, uint64_t *d_counts_u64,
-                        void *d_lo_p, hipStream_t stream) {
+// look-back tiles needed for n patterns (one per 256-pattern workgroup)
+uint64_t locate_tiles_cap(uint64_t n) { return (n + 255) / 256 > 0 ? (n + 255) / 256 : 1; }
+
+hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                        uint32_t flags, void *d_counts, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         hipLaunchKernelGGL((k_count<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, d_bytes,
-                           d_offsets, n, flags, (P *)d_counts_p, d_counts_u64, (P *)d_lo_p);
+                           d_offsets, n, flags, (P *)d_counts);
         return hipGetLastError();
     });
 }
 
-hipError_t launch_locate(const fmx_index *ix, const uint64_t *d_loc_offsets, const void *d_lo_p,
-                         uint64_t n, void *d_locs, uint64_t cap, hipStream_t stream) {
+hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
+                         uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
+                         uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
+                         hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    if ((n + 255) / 256 > tiles_cap || tiles_cap > 0xFFFFFFFFull) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
-        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, d_loc_offsets,
-                           (const P *)d_lo_p, n, (P *)d_locs, cap);
+        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, d_bytes,
+                           d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed, d_ctl,
+                           d_tiles, (uint32_t)tiles_cap);
         return hipGetLastError();
     });
 }
@@ -424,21 +532,6 @@ hipError_t launch_relayout(fmx_index *ix, hipStream_t stream) {
             return hipErrorInvalidValue;
         }
     });
-}
-
-hipError_t scan_workspace_bytes(uint64_t n, size_t *bytes) {
-    size_t b = 0;
-    hipError_t e = rocprim::exclusive_scan(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                           (uint64_t)0, (size_t)(n + 1), rocprim::plus<uint64_t>());
-    *bytes = b;
-    return e;
-}
-
-hipError_t launch_scan(const uint64_t *d_in, uint64_t *d_out, uint64_t n_plus_1, void *tmp, size_t tmp_bytes,
-                       hipStream_t stream) {
-    size_t b = tmp_bytes;
-    return rocprim::exclusive_scan(tmp, b, d_in, d_out, (uint64_t)0, (size_t)n_plus_1, rocprim::plus<uint64_t>(),
-                                   stream);
 }
 
 }  // namespace fmx

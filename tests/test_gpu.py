@@ -230,7 +230,7 @@ def test_device_async_api(pkg, O):
     d_locs = torch.zeros(cap, dtype=torch.int32, device=dev)
     d_need = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = ix.locate_workspace_size(n)
-    d_ws = torch.empty(ws, dtype=torch.uint8, device=dev)
+    d_ws = torch.zeros(ws, dtype=torch.uint8, device=dev)
     ix.locate_batch_async(d_data.data_ptr(), d_off.data_ptr(), n, d_loff.data_ptr(), d_locs.data_ptr(), cap,
                           d_need.data_ptr(), d_ws.data_ptr(), ws, d_counts=d_cnt.data_ptr())
     ix.sync()
@@ -247,7 +247,7 @@ def test_device_async_api(pkg, O):
                           d_need.data_ptr(), d_ws.data_ptr(), ws)
     ix.sync()
     t = ix.timing_read()
-    assert t["count"]["launches"] == 1 and t["locate"]["launches"] == 1 and t["count"]["total_ms"] > 0
+    assert t["locate"]["launches"] == 1 and t["locate"]["total_ms"] > 0 and t["locate"]["units"] == n
     ix.close()
 
 
