@@ -44,9 +44,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--text-len", type=int, default=1_000_000_000)
-    ap.add_argument("--patterns", type=int, default=100_000, help="patterns per GPU per step")
+    ap.add_argument("--patterns", type=int, default=100_000, help="patterns per GPU per step (weak scaling)")
+    ap.add_argument("--total-patterns", type=int, default=0,
+                    help="if > 0: one global batch sharded over the GPUs (strong scaling, e.g. C3 = 10,000,000)")
     ap.add_argument("--pattern-len", type=int, default=20)
     ap.add_argument("--occ", default="interleaved", choices=["interleaved", "blob"])
+    ap.add_argument("--no-deep-lut", action="store_true", help="do not build the device K-mer interval table")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
@@ -77,7 +80,13 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
-    n, B, m = args.text_len, args.patterns, args.pattern_len
+    D = pkg.distributed
+    n, m = args.text_len, args.pattern_len
+    if args.total_patterns > 0:
+        s0, s1 = D.shard(args.total_patterns, world, rank)
+        B = s1 - s0
+    else:
+        B = args.patterns
     # ---- synthetic text (same on every rank: the blob is replicated) -------
     t0 = time.time()
     gen = torch.Generator(device=dev)
@@ -97,9 +106,13 @@ def main():
     torch.cuda.synchronize()
     build_s = time.time() - t1
     log(f"[rank {rank}] text {n:,} B generated in {t1 - t0:.2f}s, blob {blob_len:,} B built on GPU in {build_s:.2f}s")
+    t2 = time.time()
     ix = pkg.FmIndex.load_device(d_blob.data_ptr(), blob_len, pkg.u32, block, pkg.text_encoders.EncodingTable,
-                                 device=local, occ=args.occ)
+                                 device=local, occ=args.occ, deep_lut=not args.no_deep_lut)
+    load_s = time.time() - t2
     info = ix.info()
+    log(f"[rank {rank}] index loaded in {load_s:.2f}s: options={info['options']} deep_lut_k={info['deep_lut_k']} "
+        f"device_bytes={info['device_bytes']:,}")
 
     # ---- patterns: substrings at uniform starts (per-rank seed) ------------
     pg = torch.Generator(device=dev)
@@ -146,16 +159,16 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
 
-    # ---- result concatenation across ranks (RCCL all-gather, untimed) ------
+    # ---- result concatenation across ranks (RCCL all-gathers, untimed) -----
     gather_ms = None
     if world > 1:
-        cnt = (d_loff[1:] - d_loff[:-1]).to(torch.int32)
-        outs = [torch.empty_like(cnt) for _ in range(world)]
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        dist.all_gather(outs, cnt)
+        total_local = int(d_need.item())
+        g_off, g_locs = D.concat_results(d_loff, d_locs[:total_local].to(torch.int64))
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
+        log(f"[rank {rank}] gathered {g_off.numel() - 1:,} patterns / {g_locs.numel():,} locations in {gather_ms:.2f} ms")
 
     # ---- roofline of the dominant kernel ------------------------------------
     # Algorithmic bytes: per pattern m + 2P (k-mer seed) +
@@ -179,7 +192,8 @@ def main():
     if os.path.exists(args.traffic_csv):
         try:
             pm = json.load(open(args.traffic_csv))
-            if pm.get("config") == f"{n}:{B}:{m}:{args.occ}" and dominant in pm.get("per_launch_bytes", {}):
+            cfg = f"{n}:{B}:{m}:{args.occ}:{info['deep_lut_k']}"
+            if pm.get("config") == cfg and dominant in pm.get("per_launch_bytes", {}):
                 traffic = pm["per_launch_bytes"][dominant]
                 traffic_src = os.path.relpath(args.traffic_csv, ROOT)
         except Exception:
@@ -195,7 +209,10 @@ def main():
     hit[owner[locs_h.astype(np.int64) == st_h[owner]]] = True
     self_found = bool(hit.all() and (cnt_h >= 1).all())
 
-    value = world * B * args.steps / elapsed
+    b_all = torch.tensor([B], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(b_all)
+    value = int(b_all.item()) * args.steps / elapsed
     result = {
         "metric": METRIC,
         "value": value,
@@ -205,7 +222,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.total_patterns > 0 else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic: seeded uniform ACGT text; patterns cut from it at uniform random starts",
@@ -213,6 +230,8 @@ def main():
             "workload": f"C2: {n:,} bp ACGT text (ACGTN, N wildcard), {B:,} x {m} bp patterns per GPU, "
                         f"u32/Block3<u64>/EncodingTable, SA sampling 2, k-mer LUT 3",
             "text_len": n, "patterns_per_gpu": B, "pattern_len": m, "occ_layout": args.occ,
+            "deep_lut_k": info["deep_lut_k"], "index_hbm_bytes": info["device_bytes"],
+            "global_batch": int(b_all.item()),
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
         },
         "roofline": {
@@ -225,6 +244,7 @@ def main():
         "occurrences_per_step": total_occ,
         "self_location_check": self_found,
         "build_s": build_s,
+        "load_s": load_s,
         "gather_ms": gather_ms,
     }
 

@@ -61,9 +61,16 @@ typedef struct fmx_layout {
 #define FMX_PATTERN_REVERSED 1u /* patterns are given last byte first: the *_rev_iter forms
                                    (src/locate/with_rev_iter.rs:5-38)                          */
 
-/* Device occ representation chosen at load (results are identical). */
-#define FMX_OCC_BLOB 0u        /* kernels read the blob's rank_checkpoints / blocks as laid out  */
+/* Load options: device-side structures derived from the blob at load time.
+ * Results are identical with any combination; they trade HBM for fewer
+ * dependent random reads per pattern. */
+#define FMX_OCC_BLOB 0u        /* kernels read the blob's rank_checkpoints / blocks as laid out   */
 #define FMX_OCC_INTERLEAVED 1u /* checkpoints + bit planes re-laid out into one HBM line per block */
+#define FMX_OPT_DEEP_LUT 2u    /* a K-mer interval table (K > the blob's k), built on the GPU by
+                                  breadth-first backward search; replaces the first LF steps.
+                                  K = the largest with sigma^K * 2P bytes <= FMX_DEEP_LUT_MB
+                                  (environment, default 2048) */
+#define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT)
 
 typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
 
@@ -71,12 +78,13 @@ typedef struct fmx_index_info {
     uint64_t text_len;       /* C[symbol_count]                                   */
     uint64_t sentinel_index; /* BwmView.sentinel_index                            */
     uint64_t blob_len;
-    uint64_t device_bytes;   /* HBM held by the index (blob + any re-layout)      */
+    uint64_t device_bytes;   /* HBM held by the index (blob + derived structures) */
     uint32_t symbol_count;
     uint32_t kmer_size;      /* lookup_table_kmer_size                            */
     uint32_t sampling_ratio;
     uint32_t block_len;      /* BLOCK_LEN = vec_bits                              */
-    uint32_t occ_mode;       /* FMX_OCC_*                                         */
+    uint32_t options;        /* FMX_OCC_* | FMX_OPT_* in effect                   */
+    uint32_t deep_lut_k;     /* K of the deep k-mer table (0 = none)              */
     int32_t device;
 } fmx_index_info;
 
@@ -99,15 +107,15 @@ int fmx_device_count(void);
  * consistency checks the reference leaves to the type system, then copies the
  * blob to HBM of `device` once.  The host blob is borrowed for fmx_blob() only.
  * On FMX_E_SIZE, *expected_total / *actual_total receive the two sizes.
- * occ_mode: FMX_OCC_BLOB or FMX_OCC_INTERLEAVED. */
+ * options: FMX_OCC_* | FMX_OPT_* (FMX_OPT_DEFAULT recommended). */
 fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, int device,
-                    uint32_t occ_mode, fmx_index **out, uint64_t *expected_total,
+                    uint32_t options, fmx_index **out, uint64_t *expected_total,
                     uint64_t *actual_total);
 
 /* Same, for a blob already resident in HBM of `device` (e.g. written by
  * fmx_build_device).  The device blob is borrowed and must outlive the index. */
 fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout layout, int device,
-                           uint32_t occ_mode, fmx_index **out, uint64_t *expected_total,
+                           uint32_t options, fmx_index **out, uint64_t *expected_total,
                            uint64_t *actual_total);
 
 void fmx_free(fmx_index *ix);

@@ -33,6 +33,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _native as _n
+from . import distributed  # noqa: F401  (multi-GPU helpers)
 
 __all__ = ["FmIndex", "FmIndexBuilder", "Position", "u32", "u64", "Vector", "blocks",
            "text_encoders", "build_config", "LoadError", "BuildError", "FmxError",
@@ -314,6 +315,11 @@ def _layout(position: Position, block: _Block, encoder) -> _n.fmx_layout:
     return _n.fmx_layout(position.nbytes, block.planes, block.vector.bits, encoder.ENCODER)
 
 
+def _options(occ: str, deep_lut: bool) -> int:
+    mode = _n.FMX_OCC_INTERLEAVED if occ == "interleaved" else _n.FMX_OCC_BLOB
+    return mode | (_n.FMX_OPT_DEEP_LUT if deep_lut else 0)
+
+
 def _ptr(a: Optional[np.ndarray]):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
@@ -335,11 +341,12 @@ class FmIndex:
     @classmethod
     def load(cls, blob, position: Position = u32, block: Optional[_Block] = None,
              text_encoder=text_encoders.EncodingTable, device: int = 0,
-             occ: str = "interleaved") -> "FmIndex":
+             occ: str = "interleaved", deep_lut: bool = True) -> "FmIndex":
         """``FmIndex::load`` (load_from_blob.rs:28-85): validate, then copy the
         blob to HBM once.  `occ` picks the device occ layout ("blob" reads the
         blob's arrays as they are; "interleaved" re-lays checkpoint + planes
-        into one HBM line per block).  Results are identical."""
+        into one HBM line per block); `deep_lut` builds the device K-mer
+        interval table (FMX_OPT_DEEP_LUT).  Results are identical."""
         block = block or blocks.Block2(Vector.U64)
         if isinstance(text_encoder, type):
             text_encoder = text_encoder.__new__(text_encoder)
@@ -350,7 +357,7 @@ class FmIndex:
             arr = a2
         h = C.c_void_p()
         exp, act = C.c_uint64(), C.c_uint64()
-        mode = _n.FMX_OCC_INTERLEAVED if occ == "interleaved" else _n.FMX_OCC_BLOB
+        mode = _options(occ, deep_lut)
         st = _n.lib().fmx_load(_ptr(arr), arr.size, _layout(position, block, text_encoder), device, mode,
                                C.byref(h), C.byref(exp), C.byref(act))
         if st == _n.FMX_E_FORMAT:
@@ -365,14 +372,14 @@ class FmIndex:
     @classmethod
     def load_device(cls, d_blob: int, blob_len: int, position: Position = u32,
                     block: Optional[_Block] = None, text_encoder=text_encoders.EncodingTable,
-                    device: int = 0, occ: str = "interleaved") -> "FmIndex":
+                    device: int = 0, occ: str = "interleaved", deep_lut: bool = True) -> "FmIndex":
         """Load a blob already resident in HBM (borrowed, must outlive the index)."""
         block = block or blocks.Block2(Vector.U64)
         if isinstance(text_encoder, type):
             text_encoder = text_encoder.__new__(text_encoder)
         h = C.c_void_p()
         exp, act = C.c_uint64(), C.c_uint64()
-        mode = _n.FMX_OCC_INTERLEAVED if occ == "interleaved" else _n.FMX_OCC_BLOB
+        mode = _options(occ, deep_lut)
         st = _n.lib().fmx_load_device(C.c_void_p(d_blob), blob_len, _layout(position, block, text_encoder),
                                       device, mode, C.byref(h), C.byref(exp), C.byref(act))
         if st == _n.FMX_E_FORMAT:

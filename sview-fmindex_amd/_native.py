@@ -29,6 +29,8 @@ FMX_ENC_PASS = 1
 FMX_PATTERN_REVERSED = 1
 FMX_OCC_BLOB = 0
 FMX_OCC_INTERLEAVED = 1
+FMX_OPT_DEEP_LUT = 2
+FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT
 
 
 class fmx_layout(C.Structure):
@@ -41,7 +43,7 @@ class fmx_index_info(C.Structure):
                 ("blob_len", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("symbol_count", C.c_uint32), ("kmer_size", C.c_uint32),
                 ("sampling_ratio", C.c_uint32), ("block_len", C.c_uint32),
-                ("occ_mode", C.c_uint32), ("device", C.c_int32)]
+                ("options", C.c_uint32), ("deep_lut_k", C.c_uint32), ("device", C.c_int32)]
 
 
 class fmx_kernel_timing(C.Structure):

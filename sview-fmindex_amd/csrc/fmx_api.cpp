@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -213,7 +214,7 @@ static fmx_status ensure_scratch(fmx_index *ix, uint64_t bytes) {
     return FMX_OK;
 }
 
-static fmx_status finish_load(fmx_index *ix, uint32_t occ_mode) {
+static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     QueryArgs &q = ix->qa;
     const BlobView &v = ix->bv;
     q = QueryArgs{};
@@ -236,7 +237,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t occ_mode) {
     if (hipMemset(ix->d_status, 0, 64) != hipSuccess) return FMX_E_DEVICE;
     q.status = ix->d_status;
     ix->occ_mode = FMX_OCC_BLOB;
-    if (occ_mode == FMX_OCC_INTERLEAVED) {
+    if (options & FMX_OCC_INTERLEAVED) {
         const uint32_t rec = interleaved_record_bytes(v);
         if (rec != 0) {
             ix->rec_bytes = rec;
@@ -247,6 +248,23 @@ static fmx_status finish_load(fmx_index *ix, uint32_t occ_mode) {
             ix->occ_mode = FMX_OCC_INTERLEAVED;
             if (launch_relayout(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
             if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
+        }
+    }
+    ix->options = ix->occ_mode;
+    if (options & FMX_OPT_DEEP_LUT) {
+        // the largest K with sigma^K * 2P <= budget, deeper than the blob's k
+        uint64_t budget = 2048ull << 20;
+        if (const char *env = getenv("FMX_DEEP_LUT_MB")) budget = strtoull(env, nullptr, 10) << 20;
+        const uint64_t per = 2ull * v.L.pos_bytes;
+        uint32_t K = 0;
+        uint64_t cnt = 1;
+        while (K < 32 && cnt <= budget / per / v.sigma) { cnt *= v.sigma; ++K; }
+        if (v.sigma < 2) K = 0;
+        if (K > v.k && v.n > 0) {
+            if (build_deep_lut(ix, K, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+            q.dlut = ix->d_dlut;
+            q.dlut_k = K;
+            ix->options |= FMX_OPT_DEEP_LUT;
         }
     }
     return FMX_OK;
@@ -368,6 +386,7 @@ void fmx_free(fmx_index *ix) {
     if (ix->d_scratch) hipFree(ix->d_scratch);
     if (ix->d_ws) hipFree(ix->d_ws);
     if (ix->d_occ) hipFree(ix->d_occ);
+    if (ix->d_dlut) hipFree(ix->d_dlut);
     if (ix->d_status) hipFree(ix->d_status);
     if (ix->d_blob_owned) hipFree(ix->d_blob_owned);
     if (ix->stream) hipStreamDestroy(ix->stream);
@@ -386,12 +405,13 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->text_len = ix->bv.n;
     o->sentinel_index = ix->bv.sentinel;
     o->blob_len = ix->blob_len;
-    o->device_bytes = (ix->d_blob_owned ? ix->blob_len : 0) + ix->occ_bytes;
+    o->device_bytes = (ix->d_blob_owned ? ix->blob_len : 0) + ix->occ_bytes + ix->dlut_bytes;
     o->symbol_count = ix->bv.sigma;
     o->kmer_size = ix->bv.k;
     o->sampling_ratio = ix->bv.sr;
     o->block_len = ix->bv.bl;
-    o->occ_mode = ix->occ_mode;
+    o->options = ix->options;
+    o->deep_lut_k = ix->qa.dlut_k;
     o->device = ix->device;
     return FMX_OK;
 }

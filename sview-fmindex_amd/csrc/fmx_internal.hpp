@@ -58,6 +58,9 @@ struct QueryArgs {
     uint32_t sigma, k, sr, sr_pow2_mask;  // sr_pow2_mask = sr-1 if sr is a power of two, else 0
     uint32_t strict;          // PassThrough: bytes >= sigma are an error
     uint32_t rec_bytes;       // interleaved record size
+    const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every sigma^dlut_k string, or null
+    uint32_t dlut_k;
+    uint32_t pad_;
     uint64_t C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
     uint8_t enc[256];
@@ -92,6 +95,9 @@ struct fmx_index {
     uint32_t occ_mode = FMX_OCC_BLOB;
     uint32_t rec_bytes = 0;
     uint32_t *d_status = nullptr;
+    uint8_t *d_dlut = nullptr;
+    uint64_t dlut_bytes = 0;
+    uint32_t options = 0;
     fmx::QueryArgs qa{};
     // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
@@ -119,6 +125,8 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                          hipStream_t stream);
 uint64_t locate_tiles_cap(uint64_t n);
 hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
+// Build the deep k-mer table (FMX_OPT_DEEP_LUT) for K into ix->d_dlut.
+hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream);
 uint32_t interleaved_record_bytes(const BlobView &bv);
 
 // GPU builder (fmx_build.hip).

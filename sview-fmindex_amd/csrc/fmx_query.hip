@@ -200,22 +200,41 @@ __device__ __forceinline__ uint32_t search(const QueryArgs &a, const Tables<P> &
     const P sent = (P)a.sentinel;
     lo = hi = 0;
     if (m == 0) return kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
-    // seed: count_array.rs:203-233
-    uint64_t code = 0, e, idx;
-    const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
+    uint64_t idx;
     uint32_t bad = 0;
-    for (uint64_t j = 0; j < take; ++j) {
-        const uint64_t pj = first + j;
-        const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
-        bad |= c >= sigma;
-        code += (uint64_t)(c + 1) * s.mult[j];
+    if (a.dlut != nullptr && m >= a.dlut_k) {
+        // deep k-mer table: the SA interval of the last K symbols in one read
+        // (the same interval K-k more LF steps from the blob's seed reach)
+        const uint32_t K = a.dlut_k;
+        uint64_t code = 0;
+        for (uint32_t j = 0; j < K; ++j) {
+            const uint64_t pj = m - K + j;
+            const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+            bad |= c >= sigma;
+            code = code * sigma + c;
+        }
+        if (bad) return kStatusSymbol;
+        const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
+        lo = dl[0];
+        hi = dl[1];
+        idx = m - K;
+    } else {
+        // seed: count_array.rs:203-233
+        uint64_t code = 0, e;
+        const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
+        for (uint64_t j = 0; j < take; ++j) {
+            const uint64_t pj = first + j;
+            const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+            bad |= c >= sigma;
+            code += (uint64_t)(c + 1) * s.mult[j];
+        }
+        if (bad) return kStatusSymbol;
+        if (m < k) { e = code + s.mult[m - 1] - 1; idx = 0; }
+        else { e = code; idx = m - k; }
+        const P *kt = reinterpret_cast<const P *>(a.kmer);
+        lo = kt[code - 1];
+        hi = kt[e];
     }
-    if (bad) return kStatusSymbol;
-    if (m < k) { e = code + s.mult[m - 1] - 1; idx = 0; }
-    else { e = code; idx = m - k; }
-    const P *kt = reinterpret_cast<const P *>(a.kmer);
-    lo = kt[code - 1];
-    hi = kt[e];
     // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
     while (lo < hi && idx > 0) {
         idx -= 1;
@@ -417,6 +436,43 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     }
 }
 
+// ------------------------------------------------------------ deep k-mer table
+
+// Level 1: the interval of each single symbol c is [C[c], C[c+1]) (the root,
+// the empty string, is full row 0..n which the reduced row numbering cannot
+// represent, so level 1 is written directly; count_array.rs:139-145).
+template <typename P>
+__global__ void k_dlut_root(const QueryArgs a, P *__restrict__ out) {
+    const uint32_t c = threadIdx.x;
+    if (c < a.sigma) {
+        out[2 * c] = (P)a.C[c];
+        out[2 * c + 1] = (P)a.C[c + 1];
+    }
+}
+
+// Level j -> j+1: child string cS has code c*sigma^j + code(S); its interval
+// is one LF step (next_pos_range, locate/mod.rs:39-45) from S's.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *__restrict__ parent, uint64_t np,
+                                                    P *__restrict__ child) {
+    using O = Occ<P, N, VB, REC>;
+    const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (x >= np) return;
+    const P lo = parent[2 * x], hi = parent[2 * x + 1];
+    const P sent = (P)a.sentinel;
+    for (uint32_t c = 0; c < a.sigma; ++c) {
+        P clo = 0, chi = 0;
+        if (lo < hi) {
+            const P pre = (P)a.C[c];
+            clo = pre + O::rank_at(a, lo + (lo < sent ? P(1) : P(0)), c);
+            chi = pre + O::rank_at(a, hi + (hi < sent ? P(1) : P(0)), c);
+        }
+        P *dst = child + 2 * ((uint64_t)c * np + x);
+        dst[0] = clo;
+        dst[1] = chi;
+    }
+}
+
 // -------------------------------------------------------------- k_relayout
 
 template <typename P, int N, int VB, int REC>
@@ -519,6 +575,38 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                            d_tiles, (uint32_t)tiles_cap);
         return hipGetLastError();
     });
+}
+
+hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream) {
+    const uint64_t sigma = ix->bv.sigma, pb = ix->bv.L.pos_bytes;
+    uint64_t total = 1;
+    for (uint32_t j = 0; j < K; ++j) total *= sigma;
+    uint8_t *tmp = nullptr;
+    const uint64_t tmp_entries = total / sigma;
+    hipError_t e = hipMalloc(&ix->d_dlut, total * 2 * pb);
+    if (e != hipSuccess) return e;
+    ix->dlut_bytes = total * 2 * pb;
+    if (K > 1) {
+        e = hipMalloc(&tmp, std::max<uint64_t>(tmp_entries, 1) * 2 * pb);
+        if (e != hipSuccess) return e;
+    }
+    // level j lives in the final buffer when (K - j) is even, else in tmp
+    auto buf = [&](uint32_t j) { return ((K - j) % 2 == 0) ? ix->d_dlut : tmp; };
+    QueryArgs qa = ix->qa;
+    qa.dlut = nullptr;
+    e = dispatch(ix, [&]<typename P, int N, int VB, int R>() {
+        hipLaunchKernelGGL((k_dlut_root<P>), dim3(1), dim3(64), 0, stream, qa, (P *)buf(1));
+        uint64_t np = sigma;
+        for (uint32_t j = 1; j < K; ++j) {
+            hipLaunchKernelGGL((k_dlut_level<P, N, VB, R>), dim3(grid_for(np)), dim3(256), 0, stream, qa,
+                               (const P *)buf(j), np, (P *)buf(j + 1));
+            np *= sigma;
+        }
+        return hipGetLastError();
+    });
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (tmp) hipFree(tmp);
+    return e;
 }
 
 hipError_t launch_relayout(fmx_index *ix, hipStream_t stream) {

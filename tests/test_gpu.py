@@ -13,7 +13,10 @@ from _util import (ALL_LAYOUTS, encode, occurrences, rand_chr_list, rand_pattern
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
-OCC_MODES = ("blob", "interleaved")
+# (device occ layout, deep k-mer table); a 1 MB table budget makes K > k even
+# on the small test texts (e.g. K = 8 for sigma = 4)
+OCC_MODES = (("blob", False), ("interleaved", False), ("interleaved", True))
+os.environ.setdefault("FMX_DEEP_LUT_MB", "1")
 
 
 def block_of(pkg, planes, vb):
@@ -39,7 +42,7 @@ def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True
     L = O.layout(pb, planes, vb, enc)
     orc = O.OracleIndex(blob, L)
     encoder = pkg.text_encoders.EncodingTable if enc == 0 else pkg.text_encoders.PassThrough
-    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, occ=occ)
+    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, occ=occ[0], deep_lut=occ[1])
     data, offsets = pkg.pack_patterns(pats)
     ooff, olocs = orc.locate_batch(data, offsets)
     goff, glocs = ix.locate_batch((data, offsets))
@@ -65,7 +68,7 @@ def test_readme_known_answers_gpu(pkg, O):
     b.build(g["text"].encode(), blob)
     for occ in OCC_MODES:
         fm = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64), pkg.text_encoders.EncodingTable,
-                              occ=occ)
+                              occ=occ[0], deep_lut=occ[1])
         for case in g["cases"]:
             p = case["pattern"].encode()
             if "count" in case:
@@ -87,7 +90,7 @@ def test_golden_blobs_on_gpu(pkg, O):
         blob = gpu_build(pkg, text, c["sigma"], pb, planes, vb, c["kmer_size"], c["sampling_ratio"], table)
         assert bytes(blob).hex() == c["blob"]
         for occ in OCC_MODES:
-            ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), occ=occ)
+            ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), occ=occ[0], deep_lut=occ[1])
             for q in c["queries"]:
                 p = bytes.fromhex(q["pattern"])
                 assert ix.count(p) == q["count"]
@@ -167,7 +170,8 @@ def test_repetitive_text_builder(pkg, O):
     text = b"A" * 30000 + bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=500)) + b"ACGT" * 5000
     blob = gpu_build(pkg, text, 4, 4, 2, 64, 3, 2, table)
     assert np.array_equal(blob, O.build(text, 4, O.layout(4, 2, 64), 3, 2, table))
-    check_parity(pkg, O, blob, 4, 2, 64, 0, [b"A" * 17, b"ACGTA", b"AAAC", b"TA"], "interleaved")
+    for occ in OCC_MODES:
+        check_parity(pkg, O, blob, 4, 2, 64, 0, [b"A" * 17, b"ACGTA", b"AAAC", b"TA", b"A" * 40], occ)
 
 
 def test_c1_config(pkg, O):
@@ -276,3 +280,20 @@ def test_load_device_blob(pkg, O):
     goff, glocs = ix.locate_batch((data, offsets))
     assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
     ix.close()
+
+
+def test_deep_lut_info(pkg, O):
+    """FMX_OPT_DEEP_LUT is in effect with K > k and answers like the LF path."""
+    rng = np.random.default_rng(21)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=50_000, p=[.3, .2, .2, .29, .01]).tobytes()
+    blob = gpu_build(pkg, text, 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    info = ix.info()
+    assert info["options"] & pkg._native.FMX_OPT_DEEP_LUT and info["deep_lut_k"] > 3
+    K = info["deep_lut_k"]
+    pats = [text[s:s + int(rng.integers(1, 3 * K))] for s in rng.integers(0, len(text) - 3 * K, size=3000)]
+    pats += [b"NNNNNNNNNNNNNNNN", b"A" * K, b"Z" * (K + 2)]
+    ix.close()
+    check_parity(pkg, O, blob, 4, 3, 64, 0, pats, ("interleaved", True))
+    check_parity(pkg, O, blob, 4, 3, 64, 0, pats, ("blob", True))
