@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--pattern-len", type=int, default=20)
     ap.add_argument("--occ", default="interleaved", choices=["interleaved", "blob"])
     ap.add_argument("--no-deep-lut", action="store_true", help="do not build the device K-mer interval table")
+    ap.add_argument("--options", type=int, default=-1,
+                    help="fmx_load options bit field (FMX_OCC_INTERLEAVED=1|DEEP_LUT=2|FULL_SA=4|TEXT=8); "
+                         "default: everything (minus --no-deep-lut)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
@@ -108,7 +111,8 @@ def main():
     log(f"[rank {rank}] text {n:,} B generated in {t1 - t0:.2f}s, blob {blob_len:,} B built on GPU in {build_s:.2f}s")
     t2 = time.time()
     ix = pkg.FmIndex.load_device(d_blob.data_ptr(), blob_len, pkg.u32, block, pkg.text_encoders.EncodingTable,
-                                 device=local, occ=args.occ, deep_lut=not args.no_deep_lut)
+                                 device=local, occ=args.occ, deep_lut=not args.no_deep_lut,
+                                 options=None if args.options < 0 else args.options)
     load_s = time.time() - t2
     info = ix.info()
     log(f"[rank {rank}] index loaded in {load_s:.2f}s: options={info['options']} deep_lut_k={info['deep_lut_k']} "
@@ -192,7 +196,7 @@ def main():
     if os.path.exists(args.traffic_csv):
         try:
             pm = json.load(open(args.traffic_csv))
-            cfg = f"{n}:{B}:{m}:{args.occ}:{info['deep_lut_k']}"
+            cfg = f"{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}"
             if pm.get("config") == cfg and dominant in pm.get("per_launch_bytes", {}):
                 traffic = pm["per_launch_bytes"][dominant]
                 traffic_src = os.path.relpath(args.traffic_csv, ROOT)
@@ -230,7 +234,8 @@ def main():
             "workload": f"C2: {n:,} bp ACGT text (ACGTN, N wildcard), {B:,} x {m} bp patterns per GPU, "
                         f"u32/Block3<u64>/EncodingTable, SA sampling 2, k-mer LUT 3",
             "text_len": n, "patterns_per_gpu": B, "pattern_len": m, "occ_layout": args.occ,
-            "deep_lut_k": info["deep_lut_k"], "index_hbm_bytes": info["device_bytes"],
+            "load_options": info["options"], "deep_lut_k": info["deep_lut_k"],
+            "index_hbm_bytes": info["device_bytes"],
             "global_batch": int(b_all.item()),
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
         },

@@ -70,7 +70,12 @@ typedef struct fmx_layout {
                                   breadth-first backward search; replaces the first LF steps.
                                   K = the largest with sigma^K * 2P bytes <= FMX_DEEP_LUT_MB
                                   (environment, default 2048) */
-#define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT)
+#define FMX_OPT_FULL_SA 4u     /* the full suffix array (n x P), recovered on the GPU by walking every
+                                  row to its sample: a location is one read, no walk            */
+#define FMX_OPT_TEXT 8u        /* the text (n symbol indices), recovered from the full SA; once an
+                                  interval is a single row, the rest of the pattern is compared
+                                  against the text instead of LF-stepped (needs FMX_OPT_FULL_SA) */
+#define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT)
 
 typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
 

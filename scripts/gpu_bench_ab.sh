@@ -3,6 +3,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 T=${TAG:-r1}
-timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu --no-deep-lut > gpurun_out/${T}_bench_nolut.log 2>&1 && echo nolut-ok &&
-timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu --occ blob --no-deep-lut > gpurun_out/${T}_bench_blob.log 2>&1 && echo blob-ok &&
+for O in 0 1 3 13 15; do
+  timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu --options $O > gpurun_out/${T}_bench_opt$O.log 2>&1 || exit 1
+  echo opt$O-ok
+done
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu --patterns 1000000 > gpurun_out/${T}_bench_1m.log 2>&1 && echo 1m-ok

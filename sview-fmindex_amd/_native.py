@@ -30,7 +30,9 @@ FMX_PATTERN_REVERSED = 1
 FMX_OCC_BLOB = 0
 FMX_OCC_INTERLEAVED = 1
 FMX_OPT_DEEP_LUT = 2
-FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT
+FMX_OPT_FULL_SA = 4
+FMX_OPT_TEXT = 8
+FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT
 
 
 class fmx_layout(C.Structure):

@@ -267,6 +267,16 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
             ix->options |= FMX_OPT_DEEP_LUT;
         }
     }
+    if ((options & (FMX_OPT_FULL_SA | FMX_OPT_TEXT)) && v.n > 0) {
+        if (build_full_sa(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+        q.safull = ix->d_safull;
+        ix->options |= FMX_OPT_FULL_SA;
+        if (options & FMX_OPT_TEXT) {
+            if (build_text(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+            q.text = ix->d_text;
+            ix->options |= FMX_OPT_TEXT;
+        }
+    }
     return FMX_OK;
 }
 
@@ -387,6 +397,8 @@ void fmx_free(fmx_index *ix) {
     if (ix->d_ws) hipFree(ix->d_ws);
     if (ix->d_occ) hipFree(ix->d_occ);
     if (ix->d_dlut) hipFree(ix->d_dlut);
+    if (ix->d_safull) hipFree(ix->d_safull);
+    if (ix->d_text) hipFree(ix->d_text);
     if (ix->d_status) hipFree(ix->d_status);
     if (ix->d_blob_owned) hipFree(ix->d_blob_owned);
     if (ix->stream) hipStreamDestroy(ix->stream);
@@ -405,7 +417,8 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->text_len = ix->bv.n;
     o->sentinel_index = ix->bv.sentinel;
     o->blob_len = ix->blob_len;
-    o->device_bytes = (ix->d_blob_owned ? ix->blob_len : 0) + ix->occ_bytes + ix->dlut_bytes;
+    o->device_bytes = (ix->d_blob_owned ? ix->blob_len : 0) + ix->occ_bytes + ix->dlut_bytes +
+                      (ix->d_safull ? ix->bv.n * ix->bv.L.pos_bytes : 0) + (ix->d_text ? ix->bv.n : 0);
     o->symbol_count = ix->bv.sigma;
     o->kmer_size = ix->bv.k;
     o->sampling_ratio = ix->bv.sr;

@@ -61,6 +61,8 @@ struct QueryArgs {
     const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every sigma^dlut_k string, or null
     uint32_t dlut_k;
     uint32_t pad_;
+    const uint8_t *safull;    // full suffix array [P; n] (FMX_OPT_FULL_SA), or null
+    const uint8_t *text;      // text as symbol indices [u8; n] (FMX_OPT_TEXT), or null
     uint64_t C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
     uint8_t enc[256];
@@ -97,6 +99,8 @@ struct fmx_index {
     uint32_t *d_status = nullptr;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
+    uint8_t *d_safull = nullptr;
+    uint8_t *d_text = nullptr;
     uint32_t options = 0;
     fmx::QueryArgs qa{};
     // host-API scratch (grown on demand) and its private locate workspace
@@ -127,6 +131,10 @@ uint64_t locate_tiles_cap(uint64_t n);
 hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
 // Build the deep k-mer table (FMX_OPT_DEEP_LUT) for K into ix->d_dlut.
 hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream);
+// Recover the full suffix array into ix->d_safull (FMX_OPT_FULL_SA).
+hipError_t build_full_sa(fmx_index *ix, hipStream_t stream);
+// Recover the text (symbol indices) into ix->d_text from d_safull (FMX_OPT_TEXT).
+hipError_t build_text(fmx_index *ix, hipStream_t stream);
 uint32_t interleaved_record_bytes(const BlobView &bv);
 
 // GPU builder (fmx_build.hip).

@@ -192,13 +192,20 @@ __device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s) {
 // (with_slice.rs:21-33).  Pattern position j is p[j], or p[m-1-j] when the
 // bytes were given reversed (the *_rev_iter forms, with_rev_iter.rs).
 // Returns status bits (0 = ok).
+// With the recovered text (FMX_OPT_TEXT): once the interval of P[idx..m) is
+// a single row r, P occurs at most once, at x - idx where x = SA[r]; the
+// remaining symbols P[idx-1], P[idx-2], ... (the order the LF loop would
+// consume them) are compared with T[x-1], T[x-2], ... instead of LF-stepped.
+// `res` is then set and `rloc` holds the location when the count is 1.
 template <typename P, int N, int VB, int REC>
 __device__ __forceinline__ uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p, uint64_t m,
-                                           bool rev, P &lo, P &hi) {
+                                           bool rev, P &lo, P &hi, P &rloc, bool &res) {
     using O = Occ<P, N, VB, REC>;
     const uint32_t sigma = a.sigma, k = a.k;
     const P sent = (P)a.sentinel;
     lo = hi = 0;
+    rloc = 0;
+    res = false;
     if (m == 0) return kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
     uint64_t idx;
     uint32_t bad = 0;
@@ -237,6 +244,20 @@ __device__ __forceinline__ uint32_t search(const QueryArgs &a, const Tables<P> &
     }
     // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
     while (lo < hi && idx > 0) {
+        if (a.text != nullptr && hi - lo == P(1)) {
+            const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[lo];
+            bool ok = true;
+            for (uint64_t j = idx; j-- > 0;) {
+                const uint32_t c = s.enc[p[rev ? m - 1 - j : j]];
+                if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
+                const uint64_t back = idx - j;  // T position x - back holds P[j]
+                if (back > x || a.text[x - back] != c) { ok = false; break; }
+            }
+            res = true;
+            if (ok) rloc = (P)(x - idx);
+            else hi = lo;
+            return 0;
+        }
         idx -= 1;
         const uint32_t c = s.enc[p[rev ? m - 1 - idx : idx]];
         if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
@@ -256,6 +277,7 @@ __device__ __forceinline__ uint32_t search(const QueryArgs &a, const Tables<P> &
 template <typename P, int N, int VB, int REC>
 __device__ __forceinline__ P walk_row(const QueryArgs &a, const P *C, P pos) {
     using O = Occ<P, N, VB, REC>;
+    if (a.safull != nullptr) return reinterpret_cast<const P *>(a.safull)[pos];
     const P sent = (P)a.sentinel;
     const P sr = (P)a.sr;
     const P mask = (P)a.sr_pow2_mask;
@@ -307,9 +329,10 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
     const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (i >= npat) return;
     const uint64_t beg = offs[i];
-    P lo, hi;
+    P lo, hi, rloc;
+    bool res;
     const uint32_t bad = search<P, N, VB, REC>(a, s, bytes + beg, offs[i + 1] - beg,
-                                               (flags & FMX_PATTERN_REVERSED) != 0, lo, hi);
+                                               (flags & FMX_PATTERN_REVERSED) != 0, lo, hi, rloc, res);
     if (bad) atomicOr(a.status, bad);
     out_cnt[i] = hi - lo;
 }
@@ -353,11 +376,12 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
 
     // ---- 1. SA interval of every pattern of the tile ----------------------
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
-    P lo = 0, hi = 0;
+    P lo = 0, hi = 0, rloc = 0;
+    bool res = false;
     if (i < npat) {
         const uint64_t beg = offs[i];
         const uint32_t bad = search<P, N, VB, REC>(a, s, bytes + beg, offs[i + 1] - beg,
-                                                   (flags & FMX_PATTERN_REVERSED) != 0, lo, hi);
+                                                   (flags & FMX_PATTERN_REVERSED) != 0, lo, hi, rloc, res);
         if (bad) atomicOr(a.status, bad);
         if (out_cnt) out_cnt[i] = hi - lo;
     }
@@ -429,8 +453,11 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
         }
         const P lo_j = __shfl(lo, jl);
         const uint64_t off_j = __shfl(my_off, jl);
+        const P rloc_j = __shfl(rloc, jl);
+        const int res_j = __shfl((int)res, jl);
         if (t < end) {
-            const P loc = walk_row<P, N, VB, REC>(a, s.C, lo_j + (P)(t - off_j));
+            // a pattern resolved against the text already knows its one location
+            const P loc = res_j ? rloc_j : walk_row<P, N, VB, REC>(a, s.C, lo_j + (P)(t - off_j));
             if (t < cap) out_locs[t] = loc;
         }
     }
@@ -470,6 +497,35 @@ __global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *
         P *dst = child + 2 * ((uint64_t)c * np + x);
         dst[0] = clo;
         dst[1] = chi;
+    }
+}
+
+// ------------------------------------------------ full SA and text recovery
+
+// SA[r] for every reduced row r: the locate walk of every row
+// (locate/mod.rs:19-35), done once at load.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_full_sa(const QueryArgs a, uint64_t n, P *__restrict__ sa_out) {
+    __shared__ Tables<P> s;
+    stage_tables(a, s);
+    __syncthreads();
+    QueryArgs b = a;
+    b.safull = nullptr;
+    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256)
+        sa_out[r] = walk_row<P, N, VB, REC>(b, s.C, (P)r);
+}
+
+// T[SA[r]] = first symbol of row r's suffix = the c with C[c] <= r < C[c+1].
+template <typename P>
+__global__ __launch_bounds__(256) void k_text(const QueryArgs a, uint64_t n, const P *__restrict__ sa,
+                                              uint8_t *__restrict__ text) {
+    __shared__ P sC[kMaxSigma + 1];
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
+    __syncthreads();
+    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256) {
+        uint32_t c = 0;
+        while (c + 1 < a.sigma && (uint64_t)sC[c + 1] <= r) ++c;
+        text[(uint64_t)sa[r]] = (uint8_t)c;
     }
 }
 
@@ -606,6 +662,39 @@ hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream) {
     });
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (tmp) hipFree(tmp);
+    return e;
+}
+
+static inline unsigned grid_stride_for(uint64_t n) {
+    const uint64_t g = (n + 255) / 256;
+    return (unsigned)(g < 65536 ? (g ? g : 1) : 65536);
+}
+
+hipError_t build_full_sa(fmx_index *ix, hipStream_t stream) {
+    const uint64_t n = ix->bv.n;
+    hipError_t e = hipMalloc(&ix->d_safull, std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes);
+    if (e != hipSuccess) return e;
+    e = dispatch(ix, [&]<typename P, int N, int VB, int R>() {
+        hipLaunchKernelGGL((k_full_sa<P, N, VB, R>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
+                           (P *)ix->d_safull);
+        return hipGetLastError();
+    });
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e;
+}
+
+hipError_t build_text(fmx_index *ix, hipStream_t stream) {
+    const uint64_t n = ix->bv.n;
+    hipError_t e = hipMalloc(&ix->d_text, std::max<uint64_t>(n, 1));
+    if (e != hipSuccess) return e;
+    if (ix->bv.L.pos_bytes == 4)
+        hipLaunchKernelGGL((k_text<uint32_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
+                           (const uint32_t *)ix->d_safull, ix->d_text);
+    else
+        hipLaunchKernelGGL((k_text<uint64_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
+                           (const uint64_t *)ix->d_safull, ix->d_text);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
     return e;
 }
 

@@ -13,9 +13,10 @@ from _util import (ALL_LAYOUTS, encode, occurrences, rand_chr_list, rand_pattern
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
-# (device occ layout, deep k-mer table); a 1 MB table budget makes K > k even
-# on the small test texts (e.g. K = 8 for sigma = 4)
-OCC_MODES = (("blob", False), ("interleaved", False), ("interleaved", True))
+# load options (FMX_OCC_INTERLEAVED=1 | FMX_OPT_DEEP_LUT=2 | FMX_OPT_FULL_SA=4 |
+# FMX_OPT_TEXT=8): the faithful blob path, each derived structure, everything;
+# a 1 MB table budget makes K > k even on the small test texts (K = 8 for sigma = 4)
+OCC_MODES = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8)
 os.environ.setdefault("FMX_DEEP_LUT_MB", "1")
 
 
@@ -42,7 +43,7 @@ def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True
     L = O.layout(pb, planes, vb, enc)
     orc = O.OracleIndex(blob, L)
     encoder = pkg.text_encoders.EncodingTable if enc == 0 else pkg.text_encoders.PassThrough
-    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, occ=occ[0], deep_lut=occ[1])
+    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, options=occ)
     data, offsets = pkg.pack_patterns(pats)
     ooff, olocs = orc.locate_batch(data, offsets)
     goff, glocs = ix.locate_batch((data, offsets))
@@ -68,7 +69,7 @@ def test_readme_known_answers_gpu(pkg, O):
     b.build(g["text"].encode(), blob)
     for occ in OCC_MODES:
         fm = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64), pkg.text_encoders.EncodingTable,
-                              occ=occ[0], deep_lut=occ[1])
+                              options=occ)
         for case in g["cases"]:
             p = case["pattern"].encode()
             if "count" in case:
@@ -90,7 +91,7 @@ def test_golden_blobs_on_gpu(pkg, O):
         blob = gpu_build(pkg, text, c["sigma"], pb, planes, vb, c["kmer_size"], c["sampling_ratio"], table)
         assert bytes(blob).hex() == c["blob"]
         for occ in OCC_MODES:
-            ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), occ=occ[0], deep_lut=occ[1])
+            ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=occ)
             for q in c["queries"]:
                 p = bytes.fromhex(q["pattern"])
                 assert ix.count(p) == q["count"]
@@ -290,10 +291,10 @@ def test_deep_lut_info(pkg, O):
     blob = gpu_build(pkg, text, 5, 4, 3, 64, 3, 2, table)
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
     info = ix.info()
-    assert info["options"] & pkg._native.FMX_OPT_DEEP_LUT and info["deep_lut_k"] > 3
+    assert info["options"] == pkg._native.FMX_OPT_DEFAULT and info["deep_lut_k"] > 3
     K = info["deep_lut_k"]
     pats = [text[s:s + int(rng.integers(1, 3 * K))] for s in rng.integers(0, len(text) - 3 * K, size=3000)]
     pats += [b"NNNNNNNNNNNNNNNN", b"A" * K, b"Z" * (K + 2)]
     ix.close()
-    check_parity(pkg, O, blob, 4, 3, 64, 0, pats, ("interleaved", True))
-    check_parity(pkg, O, blob, 4, 3, 64, 0, pats, ("blob", True))
+    for occ in (1 | 2, 2, 1 | 2 | 4 | 8):
+        check_parity(pkg, O, blob, 4, 3, 64, 0, pats, occ)
