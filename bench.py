@@ -1,21 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: patterns/sec (count + locate) on BASELINE.json's headline config.
 
-Workload (BASELINE.json configs[1], "C2"): 1 Gbp uniform ACGT text, symbols
-ACGTN (N = wildcard, sigma 5), layout u32 / Block3<u64> / EncodingTable,
-SA sampling 2, k-mer table k = 3; 100,000 x 20 bp patterns cut from the text at
-uniform random starts (bench/src/generate.rs:105-113, cold ratio 1.0), per GPU.
+Default workload (BASELINE.json configs[1], "C2"): 1 Gbp uniform ACGT text,
+symbols ACGTN (N = wildcard, sigma 5), layout u32 / Block3<u64> /
+EncodingTable, SA sampling 2, k-mer table k = 3; 100,000 x 20 bp patterns cut
+from the text at uniform random starts (bench/src/generate.rs:105-113, cold
+ratio 1.0), per GPU.  `--config c1|c3|c4|c5` selects the other BASELINE configs.
 
 One step = one fmx_locate_batch_async call over the batch = one launch of the
 fused k_locate kernel: k-mer seed + LF loop, single-pass look-back scan of the
-counts into output offsets, sampled-SA walk — every count (as offsets) and
-every location of every pattern, written to HBM.  Inputs (text,
-blob, patterns) are resident in HBM before the timed region.
+counts into output offsets, locations — every count (as offsets) and every
+location of every pattern, written to HBM.  Inputs (text, blob, derived index
+structures, patterns) are resident in HBM before the timed region.
 
 Multi-GPU: one process per GPU (torchrun); each rank builds its own replica of
 the blob on its GPU (deterministic), runs its own pattern batch (weak scaling,
-no collective in the timed region) and the counts are all-gathered over RCCL
-afterwards (result concatenation, timed separately).
+or a shard of --total-patterns), no collective in the timed region; the
+results are concatenated over RCCL afterwards (timed separately).
 
 Also reported: the dominant kernel's roofline (HIP events on the engine's
 stream), a CPU baseline (the oracle restatement on this host, rank 0), and a
@@ -37,17 +38,43 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "patterns/sec (count+locate), 1 Gbp text / 20 bp patterns, 1/2/4/8 MI355X"
 
+ACGTN = [b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"]
+AMINO = b"ACDEFGHIKLMNPQRSTVWY"
+CONFIGS = {
+    # BASELINE.json configs[0]: the reference's CPU-runnable plumbing case (T is the wildcard)
+    "c1": dict(text_len=1_000_000, alphabet=b"ACGT", symbols=[b"Aa", b"Cc", b"Gg", b"Tt"], pos=4, planes=2,
+               vec=64, k=3, sr=2, patterns=1_000, m=20, total=0,
+               desc="C1: 1 Mbp ACGT, 1,000 x 20 bp, u32/Block2<u64>, sr 2, k 3"),
+    # configs[1]: the headline (metric quoted on it)
+    "c2": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
+               patterns=100_000, m=20, total=0,
+               desc="C2: 1 Gbp ACGT (ACGTN, N wildcard), 100,000 x 20 bp per GPU, u32/Block3<u64>, sr 2, k 3"),
+    # configs[2]: 10 M patterns sharded over the GPUs
+    "c3": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
+               patterns=0, m=20, total=10_000_000,
+               desc="C3: 1 Gbp ACGT, 10,000,000 x 20 bp sharded over the GPUs, u32/Block3<u64>, sr 2, k 3"),
+    # configs[3]: large-alphabet occ path
+    "c4": dict(text_len=1_000_000_000, alphabet=AMINO, symbols=[bytes([c, c + 32]) for c in AMINO] + [b"Xx"],
+               pos=4, planes=5, vec=64, k=3, sr=2, patterns=100_000, m=12, total=0,
+               desc="C4: 1 G-residue protein text (20 aa + X wildcard), 100,000 x 12 aa, u32/Block5<u64>, sr 2, k 3"),
+    # configs[4]: long patterns, wide blocks, u64 positions
+    "c5": dict(text_len=3_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=8, planes=3, vec=128, k=3, sr=2,
+               patterns=0, m=150, total=1_000_000,
+               desc="C5: 3 Gbp ACGT, 1,000,000 x 150 bp sharded over the GPUs, u64/Block3<u128>, sr 2, k 3"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--text-len", type=int, default=1_000_000_000)
-    ap.add_argument("--patterns", type=int, default=100_000, help="patterns per GPU per step (weak scaling)")
-    ap.add_argument("--total-patterns", type=int, default=0,
-                    help="if > 0: one global batch sharded over the GPUs (strong scaling, e.g. C3 = 10,000,000)")
-    ap.add_argument("--pattern-len", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--text-len", type=int, default=0, help="override the config's text length")
+    ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU per step (weak scaling)")
+    ap.add_argument("--total-patterns", type=int, default=-1,
+                    help="> 0: one global batch sharded over the GPUs (strong scaling)")
+    ap.add_argument("--pattern-len", type=int, default=0)
     ap.add_argument("--occ", default="interleaved", choices=["interleaved", "blob"])
     ap.add_argument("--no-deep-lut", action="store_true", help="do not build the device K-mer interval table")
     ap.add_argument("--options", type=int, default=-1,
@@ -57,7 +84,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--traffic-csv", default=os.path.join(ROOT, "profiles", "r01_pmc_fetch_size.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_fetch_size.json"))
     return ap.parse_args()
 
 
@@ -72,6 +99,8 @@ def main():
 
     import __graft_entry__ as g
     pkg = g.load_package()
+    D = pkg.distributed
+    cfg = dict(CONFIGS[args.config])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -83,24 +112,37 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
-    D = pkg.distributed
-    n, m = args.text_len, args.pattern_len
-    if args.total_patterns > 0:
-        s0, s1 = D.shard(args.total_patterns, world, rank)
+    n = args.text_len or cfg["text_len"]
+    m = args.pattern_len or cfg["m"]
+    total = args.total_patterns if args.total_patterns >= 0 else cfg["total"]
+    if args.patterns:
+        total = 0
+    if total > 0:
+        s0, s1 = D.shard(total, world, rank)
         B = s1 - s0
     else:
-        B = args.patterns
+        B = args.patterns or cfg["patterns"]
+    P = cfg["pos"]
+    BLK = cfg["planes"] * cfg["vec"] // 8
+    pdt_t, pdt_np = (torch.int32, np.uint32) if P == 4 else (torch.int64, np.uint64)
+    position = pkg.u32 if P == 4 else pkg.u64
+    block = getattr(pkg.blocks, f"Block{cfg['planes']}")(pkg.Vector(cfg["vec"]))
+
     # ---- synthetic text (same on every rank: the blob is replicated) -------
     t0 = time.time()
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed)
-    acgt = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
-    d_text = acgt[torch.randint(0, 4, (n,), device=dev, dtype=torch.int64, generator=gen)]
-    table = pkg.text_encoders.EncodingTable.from_symbols([b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"])
-    block = pkg.blocks.Block3(pkg.Vector.U64)
-    builder = (pkg.FmIndexBuilder(n, table.symbol_count(), table, pkg.u32, block)
-               .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
-               .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    alpha = torch.tensor(list(cfg["alphabet"]), dtype=torch.uint8, device=dev)
+    d_text = torch.empty(n, dtype=torch.uint8, device=dev)
+    chunk = 1 << 28
+    for c0 in range(0, n, chunk):  # bounded int64 temporaries
+        c1 = min(n, c0 + chunk)
+        d_text[c0:c1] = alpha[torch.randint(0, len(cfg["alphabet"]), (c1 - c0,), device=dev, dtype=torch.int64,
+                                            generator=gen)]
+    table = pkg.text_encoders.EncodingTable.from_symbols(cfg["symbols"])
+    builder = (pkg.FmIndexBuilder(n, table.symbol_count(), table, position, block)
+               .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(cfg["k"]))
+               .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(cfg["sr"])))
     blob_len = builder.blob_size()
     d_blob = torch.empty(blob_len, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -110,7 +152,7 @@ def main():
     build_s = time.time() - t1
     log(f"[rank {rank}] text {n:,} B generated in {t1 - t0:.2f}s, blob {blob_len:,} B built on GPU in {build_s:.2f}s")
     t2 = time.time()
-    ix = pkg.FmIndex.load_device(d_blob.data_ptr(), blob_len, pkg.u32, block, pkg.text_encoders.EncodingTable,
+    ix = pkg.FmIndex.load_device(d_blob.data_ptr(), blob_len, position, block, pkg.text_encoders.EncodingTable,
                                  device=local, occ=args.occ, deep_lut=not args.no_deep_lut,
                                  options=None if args.options < 0 else args.options)
     load_s = time.time() - t2
@@ -126,7 +168,7 @@ def main():
     d_off = (torch.arange(B + 1, device=dev, dtype=torch.int64) * m).contiguous()
     cap = 4 * B + 4096
     d_loff = torch.zeros(B + 1, dtype=torch.int64, device=dev)
-    d_locs = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_locs = torch.zeros(cap, dtype=pdt_t, device=dev)
     d_need = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = ix.locate_workspace_size(B)
     d_ws = torch.zeros(ws, dtype=torch.uint8, device=dev)
@@ -158,18 +200,15 @@ def main():
     ix.timing_enable(False)
     ix.sync()
     timing = ix.timing_read()
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+        elapsed = D.max_over_ranks(elapsed, device=dev)
 
     # ---- result concatenation across ranks (RCCL all-gathers, untimed) -----
     gather_ms = None
     if world > 1:
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        total_local = int(d_need.item())
-        g_off, g_locs = D.concat_results(d_loff, d_locs[:total_local].to(torch.int64))
+        g_off, g_locs = D.concat_results(d_loff, d_locs[:need].to(torch.int64))
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         log(f"[rank {rank}] gathered {g_off.numel() - 1:,} patterns / {g_locs.numel():,} locations in {gather_ms:.2f} ms")
@@ -178,12 +217,11 @@ def main():
     # Algorithmic bytes: per pattern m + 2P (k-mer seed) +
     # L*2*(P+|B|) (two rank queries per LF step) + P (count), per occurrence
     # w*(P+|B|) (walk, E[w] = sr-1) + P (sampled SA) + P (location out).
-    P, BLK = 4, 24                      # u32 positions, Block3<u64> = 24 B
     k, sr = info["kmer_size"], info["sampling_ratio"]
     offs_h = d_loff.cpu().numpy().view(np.uint64)
     total_occ = int(offs_h[-1])
     # every pattern is cut from the text, so its interval never empties and the
-    # LF loop runs exactly m - k steps (with_slice.rs:27-31)
+    # LF loop of the reference runs exactly m - k steps (with_slice.rs:27-31)
     L = m - k
     per_pattern = m + 2 * P + L * 2 * (P + BLK) + P
     per_occ = (sr - 1) * (P + BLK) + 2 * P
@@ -191,21 +229,20 @@ def main():
     dominant = "locate"   # the single fused launch of a step (k_locate)
     alg_bytes = per_pattern * B + per_occ * total_occ
     achieved = alg_bytes / (kern[dominant] * 1e-3) / 1e9
-    traffic = None
-    traffic_src = None
-    if os.path.exists(args.traffic_csv):
+    traffic, traffic_src = None, None
+    key = f"{args.config}:{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}"
+    if os.path.exists(args.traffic_json):
         try:
-            pm = json.load(open(args.traffic_csv))
-            cfg = f"{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}"
-            if pm.get("config") == cfg and dominant in pm.get("per_launch_bytes", {}):
-                traffic = pm["per_launch_bytes"][dominant]
-                traffic_src = os.path.relpath(args.traffic_csv, ROOT)
+            pm = json.load(open(args.traffic_json))
+            if key in pm.get("per_launch_bytes", {}):
+                traffic = pm["per_launch_bytes"][key]
+                traffic_src = os.path.relpath(args.traffic_json, ROOT)
         except Exception:
             pass
 
     # size-independent property at full size: pattern i was cut at starts[i],
     # so starts[i] must be one of its locations
-    locs_h = d_locs[:total_occ].cpu().numpy().view(np.uint32)
+    locs_h = d_locs[:total_occ].cpu().numpy().view(pdt_np)
     st_h = starts.cpu().numpy()
     cnt_h = np.diff(offs_h).astype(np.int64)
     owner = np.repeat(np.arange(B), cnt_h)
@@ -226,17 +263,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if args.total_patterns > 0 else "weak",
+        "scaling": "strong" if total > 0 else "weak",
         "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic: seeded uniform ACGT text; patterns cut from it at uniform random starts",
+        "dtype": "u32" if P == 4 else "u64",
+        "data": f"synthetic: seeded uniform {cfg['alphabet'].decode()} text; patterns cut from it at uniform "
+                f"random starts",
         "config": {
-            "workload": f"C2: {n:,} bp ACGT text (ACGTN, N wildcard), {B:,} x {m} bp patterns per GPU, "
-                        f"u32/Block3<u64>/EncodingTable, SA sampling 2, k-mer LUT 3",
-            "text_len": n, "patterns_per_gpu": B, "pattern_len": m, "occ_layout": args.occ,
+            "workload": cfg["desc"] if (n == cfg["text_len"] and m == cfg["m"]) else
+            f"{args.config} variant: {n:,}-symbol text, {B:,} x {m} patterns per GPU",
+            "config": args.config, "text_len": n, "patterns_per_gpu": B, "pattern_len": m,
+            "global_batch": int(b_all.item()),
+            "layout": f"u{P * 8}/Block{cfg['planes']}<u{cfg['vec']}>/EncodingTable(sigma={table.symbol_count()})",
             "load_options": info["options"], "deep_lut_k": info["deep_lut_k"],
             "index_hbm_bytes": info["device_bytes"],
-            "global_batch": int(b_all.item()),
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
         },
         "roofline": {
@@ -251,6 +290,7 @@ def main():
         "build_s": build_s,
         "load_s": load_s,
         "gather_ms": gather_ms,
+        "profile_key": key,
     }
 
     # ---- CPU baseline + bit-exact check (rank 0, N=1 only) -------------------
@@ -258,8 +298,7 @@ def main():
         from oracle import oracle as O
         host_blob = O.aligned_zeros(blob_len, 16)
         host_blob[:] = d_blob.cpu().numpy()
-        L_ = O.layout(4, 3, 64, 0)
-        orc = O.OracleIndex(host_blob, L_)
+        orc = O.OracleIndex(host_blob, O.layout(P, cfg["planes"], cfg["vec"], 0))
         pats_h = d_pat.cpu().numpy()
         offs_in = np.arange(B + 1, dtype=np.uint64) * m
         # 1 thread, whole passes over the batch until the budget is spent
@@ -274,9 +313,7 @@ def main():
         tc = time.perf_counter()
         orc.locate_batch(pats_h, offs_in, threads=args.cpu_threads, cap=cap)
         cpun = B / (time.perf_counter() - tc)
-        glocs = d_locs[:total_occ].cpu().numpy().view(np.uint32)
-        exact = bool(np.array_equal(ooff, offs_h) and np.array_equal(olocs, glocs))
-        cores = os.cpu_count()
+        exact = bool(np.array_equal(ooff, offs_h) and np.array_equal(olocs, locs_h))
         try:
             model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
         except Exception:
@@ -285,7 +322,7 @@ def main():
             "value": cpu1, "unit": "patterns/s", "cores": 1, "kind": "port",
             "sample": f"{done:,} patterns = {done // B} passes over the same {B:,}-pattern batch, "
                       f"oracle/fmx_oracle.c (C restatement of the reference query path), blob in RAM",
-            f"value_{args.cpu_threads}_threads": cpun, "cpu_model": model, "host_cpus_visible": cores,
+            f"value_{args.cpu_threads}_threads": cpun, "cpu_model": model, "host_cpus_visible": os.cpu_count(),
         }
         result["parity"] = {"bit_exact_vs_cpu": exact, "patterns": B, "occurrences": total_occ}
         result["speedup_vs_cpu_1thread"] = value / cpu1

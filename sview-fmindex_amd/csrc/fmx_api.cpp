@@ -227,7 +227,10 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     q.sigma = v.sigma;
     q.k = v.k;
     q.sr = v.sr;
-    q.sr_pow2_mask = (v.sr > 1 && (v.sr & (v.sr - 1)) == 0) ? v.sr - 1 : 0;
+    q.sr_pow2 = (v.sr & (v.sr - 1)) == 0;
+    q.sr_pow2_mask = q.sr_pow2 ? v.sr - 1 : 0;
+    q.sr_shift = q.sr_pow2 ? (uint32_t)__builtin_ctz(v.sr) : 0;
+    q.sr_magic = q.sr_pow2 ? 0 : (uint64_t)((((unsigned __int128)1 << 64) + v.sr - 1) / v.sr);
     q.strict = v.L.encoder == FMX_ENC_PASS;
     memcpy(q.C, v.C, sizeof(q.C));
     memcpy(q.mult, v.mult, sizeof(q.mult));

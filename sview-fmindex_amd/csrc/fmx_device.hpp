@@ -1,0 +1,298 @@
+// fmx_device.hpp — the arithmetic of the query hot path, shared by the gfx950
+// kernels (fmx_query.hip) and a host-side emulation used by the CPU tests
+// (tests/emu): bit-plane rank/popcount, the k-mer seed, the LF loop with the
+// single-row text verification, and the sampled-SA walk.  Every function is
+// __host__ __device__ so the CPU suite runs exactly the code the GPU runs.
+#pragma once
+
+#include "fmx_internal.hpp"
+
+#define FMX_HD __host__ __device__ __forceinline__
+
+namespace fmx {
+
+// ------------------------------------------------------------------ vectors
+
+template <int VB> struct VecT;
+template <> struct VecT<32> { using W = uint32_t; static constexpr int WPP = 1; };
+template <> struct VecT<64> { using W = uint64_t; static constexpr int WPP = 1; };
+template <> struct VecT<128> { using W = uint64_t; static constexpr int WPP = 2; };  // lo, hi (little-endian u128)
+
+// The N bit planes of one BlockN<V> (components/bwm/blocks/block{2..6}.rs), held in registers.
+template <int N, int VB>
+struct Planes {
+    using W = typename VecT<VB>::W;
+    static constexpr int WPP = VecT<VB>::WPP;
+    static constexpr int WORDS = N * WPP;
+    W w[WORDS];
+
+    // Block::get_remain_count_of (block3.rs:42-55): occurrences of symbol c among
+    // the first `rem` symbols of the block (MSB-first); rem == 0 gives 0.
+    FMX_HD uint32_t rank(uint32_t rem, uint32_t c) const {
+        if constexpr (VB == 128) {
+            uint64_t lo = ~0ull, hi = ~0ull;
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const bool b = (c >> j) & 1u;
+                lo &= b ? w[2 * j] : ~w[2 * j];
+                hi &= b ? w[2 * j + 1] : ~w[2 * j + 1];
+            }
+            if (rem == 0) return 0;
+            if (rem <= 64) return (uint32_t)__builtin_popcountll(hi >> (64 - rem));
+            return (uint32_t)__builtin_popcountll(hi) + (uint32_t)__builtin_popcountll(lo >> (128 - rem));
+        } else {
+            W m = ~W(0);
+#pragma unroll
+            for (int j = 0; j < N; ++j) m &= ((c >> j) & 1u) ? w[j] : W(~w[j]);
+            if (rem == 0) return 0;
+            if constexpr (VB == 64) return (uint32_t)__builtin_popcountll(m >> (64 - rem));
+            else return (uint32_t)__builtin_popcount(m >> (32 - rem));
+        }
+    }
+
+    // Block::get_symidx_of (block3.rs:57-63): bit VB-1-rem of plane j is bit j.
+    FMX_HD uint32_t sym(uint32_t rem) const {
+        const uint32_t b = VB - 1 - rem;
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            uint32_t bit;
+            if constexpr (VB == 128) bit = b >= 64 ? (uint32_t)(w[2 * j + 1] >> (b - 64)) & 1u
+                                                   : (uint32_t)(w[2 * j] >> b) & 1u;
+            else bit = (uint32_t)(w[j] >> b) & 1u;
+            s |= bit << j;
+        }
+        return s;
+    }
+
+    FMX_HD void load(const uint8_t *p) {
+        const W *src = reinterpret_cast<const W *>(p);
+#pragma unroll
+        for (int j = 0; j < WORDS; ++j) w[j] = src[j];
+    }
+};
+
+// Select v[idx] (idx < K) with a tree of v_cndmask on the bits of idx: a
+// compare-against-constant chain gets lowered to a scratch-memory table
+// lookup by the compiler, this form stays in registers.
+template <int K, typename T>
+FMX_HD T tree_pick(const T *v, uint32_t idx) {
+    if constexpr (K == 1) {
+        return v[0];
+    } else {
+        const T lo = tree_pick<K / 2>(v, idx);
+        const T hi = tree_pick<K / 2>(v + K / 2, idx);
+        return (idx & (K / 2)) ? hi : lo;
+    }
+}
+
+constexpr int pow2_ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
+
+FMX_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// pos / sr and pos % sr for the SA sampling ratio: a shift for powers of two,
+// else a multiply-high by ceil(2^64/sr) and one correction — branch-free, so a
+// wavefront whose lanes walk different rows stays converged (the generic
+// 64-bit divide expands into divergent branches).
+FMX_HD uint64_t sr_div(const QueryArgs &a, uint64_t pos, uint64_t &rem) {
+    if (a.sr_pow2) {
+        rem = pos & a.sr_pow2_mask;
+        return pos >> a.sr_shift;
+    }
+    uint64_t q = mulhi64(pos, a.sr_magic);
+    const uint64_t qd = q * a.sr;
+    q = qd > pos ? q - 1 : q;
+    rem = pos - q * a.sr;
+    return q;
+}
+
+// ------------------------------------------------------- occ access (rank)
+
+// REC == 0 — blob layout: rank_checkpoints [P; blocks*sigma] and blocks
+//            [BlockN<V>; blocks] are separate arrays (bwm/mod.rs:145-190).
+// REC > 0  — interleaved layout: record q (REC = 64 or 128 bytes, aligned) is
+//            [ckpt[0..sigma) as P][pad][bit planes at REC - N*VB/8], so one
+//            LF step reads one HBM line.
+template <typename P, int N, int VB, int REC>
+struct Occ {
+    static constexpr int PLANE_BYTES = N * VB / 8;
+    static constexpr int PLANE_OFF = REC - PLANE_BYTES;
+    static constexpr int NCK = REC == 0 ? (1 << N) : PLANE_OFF / (int)sizeof(P);  // checkpoint slots
+    static constexpr int NCK2 = pow2_ceil(NCK);
+
+    // Occ(c, stored position p): BwmView::get_next_rank after the sentinel
+    // adjustment (bwm/mod.rs:206-214).  c is known before the loads, so only
+    // the planes and the one checkpoint are fetched, all independently.
+    FMX_HD static P rank_at(const QueryArgs &a, P p, uint32_t c) {
+        const uint64_t q = (uint64_t)p / VB;
+        const uint32_t rem = (uint32_t)((uint64_t)p % VB);
+        Planes<N, VB> pl;
+        P ck;
+        if constexpr (REC == 0) {
+            ck = reinterpret_cast<const P *>(a.ckpt)[q * a.sigma + c];
+            pl.load(a.blocks + q * PLANE_BYTES);
+        } else {
+            const uint8_t *r = a.occ + q * REC;
+            ck = reinterpret_cast<const P *>(r)[c];
+            pl.load(r + PLANE_OFF);
+        }
+        return ck + (P)pl.rank(rem, c);
+    }
+
+    // get_pre_rank_and_symidx body (bwm/mod.rs:223-235) for stored position p:
+    // the symbol is only known after the planes arrive, so every checkpoint
+    // slot of the block is fetched alongside them (one round trip) and the
+    // right one selected in registers.
+    FMX_HD static P pre_rank_sym(const QueryArgs &a, P p, uint32_t &c) {
+        const uint64_t q = (uint64_t)p / VB;
+        const uint32_t rem = (uint32_t)((uint64_t)p % VB);
+        Planes<N, VB> pl;
+        if constexpr (REC == 0) {
+            pl.load(a.blocks + q * PLANE_BYTES);
+            const P *ckq = reinterpret_cast<const P *>(a.ckpt) + q * a.sigma;
+            if constexpr (N <= 3) {
+                P all[NCK2];
+#pragma unroll
+                for (int i = 0; i < NCK2; ++i) all[i] = (uint32_t)i < a.sigma ? ckq[i] : P(0);
+                c = pl.sym(rem);
+                return tree_pick<NCK2>(all, c) + (P)pl.rank(rem, c);
+            } else {
+                c = pl.sym(rem);
+                return ckq[c] + (P)pl.rank(rem, c);
+            }
+        } else {
+            const uint8_t *r = a.occ + q * REC;
+            P all[NCK2];
+            const P *ckr = reinterpret_cast<const P *>(r);
+#pragma unroll
+            for (int i = 0; i < NCK2; ++i) all[i] = i < NCK ? ckr[i] : P(0);
+            pl.load(r + PLANE_OFF);
+            c = pl.sym(rem);
+            return tree_pick<NCK2>(all, c) + (P)pl.rank(rem, c);
+        }
+    }
+};
+
+// ----------------------------------------------------- shared kernel parts
+
+template <typename P>
+struct Tables {
+    uint8_t enc[256];
+    P C[kMaxSigma + 1];
+    uint64_t mult[kMaxK];
+};
+
+// k-mer seed + LF loop for pattern bytes p[0..m): FmIndex::get_pos_range
+// (with_slice.rs:21-33).  Pattern position j is p[j], or p[m-1-j] when the
+// bytes were given reversed (the *_rev_iter forms, with_rev_iter.rs).
+// Returns status bits (0 = ok).
+// With the recovered text (FMX_OPT_TEXT): once the interval of P[idx..m) is
+// a single row r, P occurs at most once, at x - idx where x = SA[r]; the
+// remaining symbols P[idx-1], P[idx-2], ... (the order the LF loop would
+// consume them) are compared with T[x-1], T[x-2], ... instead of LF-stepped.
+// `res` is then set and `rloc` holds the location when the count is 1.
+template <typename P, int N, int VB, int REC>
+FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p, uint64_t m,
+                                           bool rev, P &lo, P &hi, P &rloc, bool &res) {
+    using O = Occ<P, N, VB, REC>;
+    const uint32_t sigma = a.sigma, k = a.k;
+    const P sent = (P)a.sentinel;
+    lo = hi = 0;
+    rloc = 0;
+    res = false;
+    if (m == 0) return kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
+    uint64_t idx;
+    uint32_t bad = 0;
+    if (a.dlut != nullptr && m >= a.dlut_k) {
+        // deep k-mer table: the SA interval of the last K symbols in one read
+        // (the same interval K-k more LF steps from the blob's seed reach)
+        const uint32_t K = a.dlut_k;
+        uint64_t code = 0;
+        for (uint32_t j = 0; j < K; ++j) {
+            const uint64_t pj = m - K + j;
+            const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+            bad |= c >= sigma;
+            code = code * sigma + c;
+        }
+        if (bad) return kStatusSymbol;
+        const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
+        lo = dl[0];
+        hi = dl[1];
+        idx = m - K;
+    } else {
+        // seed: count_array.rs:203-233
+        uint64_t code = 0, e;
+        const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
+        for (uint64_t j = 0; j < take; ++j) {
+            const uint64_t pj = first + j;
+            const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+            bad |= c >= sigma;
+            code += (uint64_t)(c + 1) * s.mult[j];
+        }
+        if (bad) return kStatusSymbol;
+        if (m < k) { e = code + s.mult[m - 1] - 1; idx = 0; }
+        else { e = code; idx = m - k; }
+        const P *kt = reinterpret_cast<const P *>(a.kmer);
+        lo = kt[code - 1];
+        hi = kt[e];
+    }
+    // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
+    while (lo < hi && idx > 0) {
+        if (a.text != nullptr && hi - lo == P(1)) {
+            const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[lo];
+            bool ok = true;
+            for (uint64_t j = idx; j-- > 0;) {
+                const uint32_t c = s.enc[p[rev ? m - 1 - j : j]];
+                if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
+                const uint64_t back = idx - j;  // T position x - back holds P[j]
+                if (back > x || a.text[x - back] != c) { ok = false; break; }
+            }
+            res = true;
+            if (ok) rloc = (P)(x - idx);
+            else hi = lo;
+            return 0;
+        }
+        idx -= 1;
+        const uint32_t c = s.enc[p[rev ? m - 1 - idx : idx]];
+        if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
+        const P plo = lo + (lo < sent ? P(1) : P(0));  // bwm/mod.rs:202-204
+        const P phi = hi + (hi < sent ? P(1) : P(0));
+        const P rlo = O::rank_at(a, plo, c);
+        const P rhi = O::rank_at(a, phi, c);
+        const P pre = s.C[c];
+        lo = pre + rlo;
+        hi = pre + rhi;
+    }
+    return 0;
+}
+
+// Walk one suffix-array row to a sampled row or to the text start
+// (locate/mod.rs:19-35; suffix_array/mod.rs:100-105).
+template <typename P, int N, int VB, int REC>
+FMX_HD P walk_row(const QueryArgs &a, const P *C, P pos) {
+    using O = Occ<P, N, VB, REC>;
+    if (a.safull != nullptr) return reinterpret_cast<const P *>(a.safull)[pos];
+    const P sent = (P)a.sentinel;
+    P off = 0;
+    uint64_t rem;
+    uint64_t slot = sr_div(a, (uint64_t)pos, rem);
+    while (rem != 0) {
+        if (pos == (P)(sent - P(1))) return off;  // get_pre_rank_and_symidx -> None
+        const P p = pos + (pos < sent ? P(1) : P(0));
+        uint32_t c;
+        const P rank = O::pre_rank_sym(a, p, c);
+        pos = C[c] + rank;
+        off += 1;
+        slot = sr_div(a, (uint64_t)pos, rem);
+    }
+    return reinterpret_cast<const P *>(a.sa)[slot] + off;
+}
+
+
+}  // namespace fmx

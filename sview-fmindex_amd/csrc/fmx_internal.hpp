@@ -56,6 +56,8 @@ struct QueryArgs {
     uint32_t *status;         // latched device status bits
     uint64_t n, sentinel;
     uint32_t sigma, k, sr, sr_pow2_mask;  // sr_pow2_mask = sr-1 if sr is a power of two, else 0
+    uint32_t sr_pow2, sr_shift;          // sr is a power of two (1 included), log2(sr)
+    uint64_t sr_magic;                   // ceil(2^64 / sr) for sr not a power of two
     uint32_t strict;          // PassThrough: bytes >= sigma are an error
     uint32_t rec_bytes;       // interleaved record size
     const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every sigma^dlut_k string, or null

@@ -1,0 +1,182 @@
+// TEST INFRASTRUCTURE — host emulation of the query kernels.
+//
+// Runs the engine's own __host__ __device__ arithmetic
+// (sview-fmindex_amd/csrc/fmx_device.hpp: rank/popcount, seed, LF loop,
+// single-row text verification, walk) on the CPU, one pattern at a time, over
+// the same derived structures the loader builds on the GPU (interleaved occ
+// records, deep k-mer table, full SA, text), so the CPU test suite checks the
+// device code paths against the oracle without a GPU.  Blob offsets come from
+// the oracle's parser (oracle/fmx_oracle.c).
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../sview-fmindex_amd/csrc/fmx_device.hpp"
+#include "../../oracle/fmx_oracle.h"
+
+using namespace fmx;
+
+namespace {
+
+template <typename P, int N, int VB, int REC>
+int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
+        uint32_t flags, uint64_t *counts, uint64_t *locs, uint64_t cap, uint64_t *needed) {
+    QueryArgs a{};
+    const uint8_t *blob = ox.blob;
+    a.ckpt = blob + ox.off_ckpt;
+    a.blocks = blob + ox.off_blocks;
+    a.sa = blob + ox.off_sa;
+    a.kmer = blob + ox.off_kmer;
+    a.n = ox.n;
+    a.sentinel = ox.sentinel;
+    a.sigma = ox.sigma;
+    a.k = ox.k;
+    a.sr = ox.sr;
+    a.sr_pow2 = (ox.sr & (ox.sr - 1)) == 0;
+    a.sr_pow2_mask = a.sr_pow2 ? ox.sr - 1 : 0;
+    a.sr_shift = a.sr_pow2 ? (uint32_t)__builtin_ctz(ox.sr) : 0;
+    a.sr_magic = a.sr_pow2 ? 0 : (uint64_t)((((unsigned __int128)1 << 64) + ox.sr - 1) / ox.sr);
+    a.strict = ox.L.encoder == 1;
+    for (uint32_t c = 0; c <= ox.sigma; ++c) a.C[c] = ox.count_array[c];
+    for (uint32_t i = 0; i < ox.k && i < (uint32_t)kMaxK; ++i) a.mult[i] = ox.mult[i];
+    memcpy(a.enc, ox.enc, 256);
+    Tables<P> t{};
+    memcpy(t.enc, ox.enc, 256);
+    for (uint32_t c = 0; c <= ox.sigma; ++c) t.C[c] = (P)ox.count_array[c];
+    for (uint32_t i = 0; i < ox.k && i < (uint32_t)kMaxK; ++i) t.mult[i] = ox.mult[i];
+
+    // interleaved records (k_relayout)
+    std::vector<uint8_t> occ;
+    if constexpr (REC != 0) {
+        constexpr int PB = N * VB / 8;
+        occ.assign(ox.blocks_len * REC + 16, 0);
+        for (uint64_t q = 0; q < ox.blocks_len; ++q) {
+            memcpy(&occ[q * REC], a.ckpt + q * ox.sigma * sizeof(P), ox.sigma * sizeof(P));
+            memcpy(&occ[q * REC + REC - PB], a.blocks + q * PB, PB);
+        }
+        a.occ = occ.data();
+    }
+    using O = Occ<P, N, VB, REC>;
+    // deep k-mer table (k_dlut_root / k_dlut_level)
+    std::vector<P> lut, lev;
+    if (options & 2u) {
+        uint64_t budget = 1ull << 20;  // what tests/test_gpu.py sets (FMX_DEEP_LUT_MB=1)
+        uint32_t K = 0;
+        uint64_t cnt = 1;
+        while (K < 32 && cnt <= budget / (2 * sizeof(P)) / ox.sigma) { cnt *= ox.sigma; ++K; }
+        if (ox.sigma >= 2 && K > ox.k && ox.n > 0) {
+            lev.assign(2 * ox.sigma, 0);
+            for (uint32_t c = 0; c < ox.sigma; ++c) { lev[2 * c] = (P)a.C[c]; lev[2 * c + 1] = (P)a.C[c + 1]; }
+            uint64_t np = ox.sigma;
+            for (uint32_t j = 1; j < K; ++j) {
+                std::vector<P> nxt(2 * np * ox.sigma, 0);
+                for (uint64_t x = 0; x < np; ++x) {
+                    const P lo = lev[2 * x], hi = lev[2 * x + 1];
+                    if (!(lo < hi)) continue;
+                    for (uint32_t c = 0; c < ox.sigma; ++c) {
+                        const P pre = (P)a.C[c];
+                        nxt[2 * (c * np + x)] = pre + O::rank_at(a, lo + (lo < (P)a.sentinel ? P(1) : P(0)), c);
+                        nxt[2 * (c * np + x) + 1] = pre + O::rank_at(a, hi + (hi < (P)a.sentinel ? P(1) : P(0)), c);
+                    }
+                }
+                lev.swap(nxt);
+                np *= ox.sigma;
+            }
+            lut.swap(lev);
+            a.dlut = reinterpret_cast<const uint8_t *>(lut.data());
+            a.dlut_k = K;
+        }
+    }
+    // full SA (k_full_sa) and text (k_text)
+    std::vector<P> safull;
+    std::vector<uint8_t> text;
+    if ((options & (4u | 8u)) && ox.n > 0) {
+        safull.resize(ox.n);
+        for (uint64_t r = 0; r < ox.n; ++r) safull[r] = walk_row<P, N, VB, REC>(a, t.C, (P)r);
+        a.safull = reinterpret_cast<const uint8_t *>(safull.data());
+        if (options & 8u) {
+            text.assign(ox.n, 0);
+            for (uint64_t r = 0; r < ox.n; ++r) {
+                uint32_t c = 0;
+                while (c + 1 < ox.sigma && (uint64_t)t.C[c + 1] <= r) ++c;
+                text[(uint64_t)safull[r]] = (uint8_t)c;
+            }
+            a.text = text.data();
+        }
+    }
+    // queries (k_locate without the scan: outputs are in pattern order anyway)
+    uint64_t out = 0;
+    for (uint64_t i = 0; i < npat; ++i) {
+        P lo, hi, rloc;
+        bool res;
+        const uint32_t bad = search<P, N, VB, REC>(a, t, bytes + offs[i], offs[i + 1] - offs[i],
+                                                   (flags & 1u) != 0, lo, hi, rloc, res);
+        if (bad) return bad == kStatusEmpty ? ORC_E_EMPTY_PATTERN : ORC_E_SYMBOL;
+        const uint64_t cnt = (uint64_t)(hi - lo);
+        counts[i] = cnt;
+        for (uint64_t j = 0; j < cnt; ++j, ++out) {
+            const P loc = res ? rloc : walk_row<P, N, VB, REC>(a, t.C, lo + (P)j);
+            if (out < cap) locs[out] = (uint64_t)loc;
+        }
+    }
+    *needed = out;
+    return out > cap ? ORC_E_CAPACITY : ORC_OK;
+}
+
+template <typename P, int N, int VB>
+int by_rec(uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b, const uint64_t *o, uint64_t n,
+           uint32_t f, uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need) {
+    if (rec == 64) {
+        if constexpr (N * VB / 8 + (int)sizeof(P) <= 64) return run<P, N, VB, 64>(ox, options, b, o, n, f, c, l, cap, need);
+        return -1;
+    }
+    if (rec == 128) {
+        if constexpr (N * VB / 8 + (int)sizeof(P) <= 128) return run<P, N, VB, 128>(ox, options, b, o, n, f, c, l, cap, need);
+        return -1;
+    }
+    return run<P, N, VB, 0>(ox, options, b, o, n, f, c, l, cap, need);
+}
+
+template <typename P, int N>
+int by_vb(uint32_t vb, uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b, const uint64_t *o,
+          uint64_t n, uint32_t f, uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need) {
+    if (vb == 32) return by_rec<P, N, 32>(rec, ox, options, b, o, n, f, c, l, cap, need);
+    if (vb == 64) return by_rec<P, N, 64>(rec, ox, options, b, o, n, f, c, l, cap, need);
+    return by_rec<P, N, 128>(rec, ox, options, b, o, n, f, c, l, cap, need);
+}
+
+template <typename P>
+int by_n(const orc_index &ox, uint32_t rec, uint32_t options, const uint8_t *b, const uint64_t *o, uint64_t n,
+         uint32_t f, uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need) {
+    switch (ox.L.planes) {
+        case 2: return by_vb<P, 2>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
+        case 3: return by_vb<P, 3>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
+        case 4: return by_vb<P, 4>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
+        case 5: return by_vb<P, 5>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
+        default: return by_vb<P, 6>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text).
+// Outputs are u64: counts[npat] and the concatenated locations.
+int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
+               uint32_t encoder, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
+               uint32_t flags, uint64_t *counts, uint64_t *locs, uint64_t cap, uint64_t *needed) {
+    orc_layout L{pos_bytes, planes, vec_bits, encoder};
+    orc_index ox;
+    int st = orc_load(blob, len, L, &ox, nullptr, nullptr);
+    if (st) return st;
+    uint32_t rec = 0;
+    if (options & 1u) {
+        const uint32_t need = planes * vec_bits / 8 + ox.sigma * pos_bytes;
+        rec = need <= 64 ? 64 : (need <= 128 ? 128 : 0);
+    }
+    if (pos_bytes == 4) return by_n<uint32_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
+    return by_n<uint64_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
+}
+
+}  // extern "C"

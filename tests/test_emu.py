@@ -1,0 +1,88 @@
+"""CPU tests of the kernels' arithmetic: tests/emu/libfmx_emu.so runs the
+engine's __host__ __device__ code (sview-fmindex_amd/csrc/fmx_device.hpp —
+rank/popcount for every Block x Vector, seed, LF loop, deep k-mer table, full
+SA, single-row text verification, walk) on the CPU, and every count and
+location (SA-row order) is compared with the oracle.  The GPU tests
+(test_gpu.py) run the same code on the device."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from _util import ALL_LAYOUTS, rand_chr_list, rand_pattern, rand_text, table_from_symbols
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EMU = os.path.join(HERE, "emu", "libfmx_emu.so")
+OPTIONS = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 2 | 8)
+
+
+@pytest.fixture(scope="module")
+def emu():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "emu")])
+    lib = C.CDLL(EMU)
+    u32, u64, p = C.c_uint32, C.c_uint64, C.c_void_p
+    lib.emu_locate.argtypes = [p, u64, u32, u32, u32, u32, u32, p, p, u64, u32, p, p, u64, C.POINTER(u64)]
+    lib.emu_locate.restype = C.c_int
+    return lib
+
+
+def emu_locate(lib, blob, layout, options, pats, reverse=False):
+    pb, planes, vb, enc = layout
+    data = np.frombuffer(b"".join(pats), np.uint8) if pats else np.zeros(1, np.uint8)
+    offs = np.zeros(len(pats) + 1, np.uint64)
+    np.cumsum([len(x) for x in pats], out=offs[1:])
+    counts = np.zeros(max(len(pats), 1), np.uint64)
+    cap = 1 << 20
+    locs = np.zeros(cap, np.uint64)
+    need = C.c_uint64()
+    st = lib.emu_locate(blob.ctypes.data, blob.size, pb, planes, vb, enc, options, data.ctypes.data,
+                        offs.ctypes.data, len(pats), 1 if reverse else 0, counts.ctypes.data, locs.ctypes.data,
+                        cap, C.byref(need))
+    return st, counts[:len(pats)], locs[:need.value]
+
+
+def check(lib, O, blob, layout, pats, options):
+    L = O.layout(*layout)
+    orc = O.OracleIndex(blob, L)
+    data = np.frombuffer(b"".join(pats), np.uint8)
+    offs = np.zeros(len(pats) + 1, np.uint64)
+    np.cumsum([len(x) for x in pats], out=offs[1:])
+    ooff, olocs = orc.locate_batch(data, offs)
+    st, cnt, locs = emu_locate(lib, blob, layout, options, pats)
+    assert st == 0
+    assert np.array_equal(cnt, np.diff(ooff)), f"counts differ, options={options}"
+    assert np.array_equal(locs, olocs.astype(np.uint64)), f"locations differ, options={options}"
+    st, rcnt, rlocs = emu_locate(lib, blob, layout, options, [x[::-1] for x in pats], reverse=True)
+    assert st == 0 and np.array_equal(rcnt, cnt) and np.array_equal(rlocs, locs)
+
+
+@pytest.mark.parametrize("pb,planes,vb", ALL_LAYOUTS)
+def test_device_code_every_layout(emu, O, pb, planes, vb):
+    rng = np.random.default_rng(pb * 1000 + planes * 100 + vb)
+    for sigma in sorted({2, 3, (1 << planes) // 2 + 1, 1 << planes}):
+        chars = rand_chr_list(rng, sigma)
+        table = table_from_symbols([bytes([c]) for c in chars])
+        text = rand_text(rng, chars, 300, 2000)
+        k, sr = int(rng.integers(1, 5)), int(rng.integers(1, 5))
+        if (sigma + 1) ** k > 1 << 20:
+            k = 2
+        blob = O.build(text, sigma, O.layout(pb, planes, vb), k, sr, table)
+        pats = [rand_pattern(rng, text, 1, 24) for _ in range(200)]
+        pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=int(rng.integers(1, 12))))
+                 for _ in range(30)]
+        pats += [b"\x00", b"\x7f\x7f", chars[:1] * 2]
+        for options in OPTIONS:
+            check(emu, O, blob, (pb, planes, vb, 0), pats, options)
+
+
+def test_device_code_repetitive(emu, O):
+    table = table_from_symbols([b"A", b"C", b"G", b"T"])
+    text = b"AC" * 3000 + b"GT" * 40 + b"A" * 2000
+    pats = [b"A", b"AC", b"CA", b"ACA", b"G", b"GT", b"TA", b"AAAA", b"A" * 30, b"CA" * 12 + b"G"]
+    for layout in [(4, 2, 64, 0), (8, 3, 128, 0), (8, 2, 64, 0)]:
+        for sr in (1, 2, 3, 5):
+            blob = O.build(text, 4, O.layout(*layout[:3]), 3, sr, table)
+            for options in OPTIONS:
+                check(emu, O, blob, layout, pats, options)
