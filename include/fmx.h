@@ -69,7 +69,7 @@ typedef struct fmx_layout {
 #define FMX_OPT_DEEP_LUT 2u    /* a K-mer interval table (K > the blob's k), built on the GPU by
                                   breadth-first backward search; replaces the first LF steps.
                                   K = the largest with sigma^K * 2P bytes <= FMX_DEEP_LUT_MB
-                                  (environment, default 2048) */
+                                  (environment, default 16384) */
 #define FMX_OPT_FULL_SA 4u     /* the full suffix array (n x P), recovered on the GPU by walking every
                                   row to its sample: a location is one read, no walk            */
 #define FMX_OPT_TEXT 8u        /* the text (n symbol indices), recovered from the full SA; once an

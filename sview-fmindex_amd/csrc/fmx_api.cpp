@@ -256,7 +256,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     ix->options = ix->occ_mode;
     if (options & FMX_OPT_DEEP_LUT) {
         // the largest K with sigma^K * 2P <= budget, deeper than the blob's k
-        uint64_t budget = 2048ull << 20;
+        uint64_t budget = 16384ull << 20;
         if (const char *env = getenv("FMX_DEEP_LUT_MB")) budget = strtoull(env, nullptr, 10) << 20;
         const uint64_t per = 2ull * v.L.pos_bytes;
         uint32_t K = 0;

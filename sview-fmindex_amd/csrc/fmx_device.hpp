@@ -188,20 +188,63 @@ struct Tables {
     uint64_t mult[kMaxK];
 };
 
-// k-mer seed + LF loop for pattern bytes p[0..m): FmIndex::get_pos_range
-// (with_slice.rs:21-33).  Pattern position j is p[j], or p[m-1-j] when the
-// bytes were given reversed (the *_rev_iter forms, with_rev_iter.rs).
-// Returns status bits (0 = ok).
-// With the recovered text (FMX_OPT_TEXT): once the interval of P[idx..m) is
-// a single row r, P occurs at most once, at x - idx where x = SA[r]; the
-// remaining symbols P[idx-1], P[idx-2], ... (the order the LF loop would
-// consume them) are compared with T[x-1], T[x-2], ... instead of LF-stepped.
-// `res` is then set and `rloc` holds the location when the count is 1.
+// One pattern, position j = 0..m-1 in pattern order.  Either staged: the
+// encoded symbols in LDS (the workgroup copies its patterns' bytes once,
+// through the encoding table, reversed for *_rev_iter input), or raw: the
+// input bytes in HBM, encoded on each access.
+struct PatView {
+    const uint8_t *sym;  // staged symbols (pattern order), or null
+    const uint8_t *raw;  // raw bytes (input order)
+    const uint8_t *enc;  // encoding table
+    uint64_t m;
+    bool rev;
+    FMX_HD uint32_t at(uint64_t j) const { return sym ? sym[j] : enc[raw[rev ? m - 1 - j : j]]; }
+};
+
+// Four text symbols t[a..a+4) from two aligned words (the text buffer is
+// padded by 16 bytes past n).
+FMX_HD uint32_t load4(const uint8_t *t, uint64_t a) {
+    const uint64_t al = a & ~3ull;
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t *>(t + al);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(t + al + 4);
+    return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+}
+
+// Single-row tail (FMX_OPT_TEXT): the interval of P[idx..m) is the one row
+// whose suffix starts at text position x, so P occurs at most once, at
+// x - idx.  The LF loop would consume P[idx-1], P[idx-2], ... and stop at the
+// first symbol that does not precede the suffix (or at the text start); here
+// the same positions are compared with T[x-1], T[x-2], ... four at a time.
+// Returns the highest position jm that fails (-1: P occurs at x - idx).
+template <typename P>
+FMX_HD int64_t tail_mismatch(const QueryArgs &a, const PatView &pv, uint64_t idx, uint64_t x) {
+    const uint64_t lowest = idx > x ? idx - x : 0;  // positions below have no text before them
+    const uint64_t tb = x - idx;                     // text position of P[0] (mod 2^64)
+    uint64_t hj = idx;
+    while (hj > lowest) {
+        const uint64_t lj = hj - lowest >= 4 ? hj - 4 : lowest;
+        const uint32_t tw = load4(a.text, tb + lj);
+        uint32_t mism = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+            if (lj + u < hj && ((tw >> (8 * u)) & 0xffu) != pv.at(lj + u)) mism |= 1u << u;
+        if (mism) return (int64_t)(lj + (31 - __builtin_clz(mism)));
+        hj = lj;
+    }
+    return lowest > 0 ? (int64_t)(lowest - 1) : -1;
+}
+
+// k-mer seed + LF loop: FmIndex::get_pos_range (with_slice.rs:21-33).
+// Returns status bits (0 = ok).  With the recovered text, a single-row
+// interval ends the loop through tail_mismatch; `res` is then set and `rloc`
+// holds the location when the count is 1.
 template <typename P, int N, int VB, int REC>
-FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p, uint64_t m,
-                                           bool rev, P &lo, P &hi, P &rloc, bool &res) {
+FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv, P &lo, P &hi, P &rloc,
+                       bool &res) {
     using O = Occ<P, N, VB, REC>;
     const uint32_t sigma = a.sigma, k = a.k;
+    const uint64_t m = pv.m;
     const P sent = (P)a.sentinel;
     lo = hi = 0;
     rloc = 0;
@@ -214,9 +257,9 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p,
         // (the same interval K-k more LF steps from the blob's seed reach)
         const uint32_t K = a.dlut_k;
         uint64_t code = 0;
+#pragma unroll 4
         for (uint32_t j = 0; j < K; ++j) {
-            const uint64_t pj = m - K + j;
-            const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+            const uint32_t c = pv.at(m - K + j);
             bad |= c >= sigma;
             code = code * sigma + c;
         }
@@ -230,8 +273,7 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p,
         uint64_t code = 0, e;
         const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
         for (uint64_t j = 0; j < take; ++j) {
-            const uint64_t pj = first + j;
-            const uint32_t c = s.enc[p[rev ? m - 1 - pj : pj]];
+            const uint32_t c = pv.at(first + j);
             bad |= c >= sigma;
             code += (uint64_t)(c + 1) * s.mult[j];
         }
@@ -243,29 +285,30 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const uint8_t *p,
         hi = kt[e];
     }
     // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
+    uint32_t c = idx > 0 ? pv.at(idx - 1) : 0;  // next symbol, fetched one step ahead
     while (lo < hi && idx > 0) {
         if (a.text != nullptr && hi - lo == P(1)) {
             const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[lo];
-            bool ok = true;
-            for (uint64_t j = idx; j-- > 0;) {
-                const uint32_t c = s.enc[p[rev ? m - 1 - j : j]];
-                if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
-                const uint64_t back = idx - j;  // T position x - back holds P[j]
-                if (back > x || a.text[x - back] != c) { ok = false; break; }
-            }
+            const int64_t jm = tail_mismatch<P>(a, pv, idx, x);
             res = true;
-            if (ok) rloc = (P)(x - idx);
-            else hi = lo;
+            if (jm >= 0) {
+                // the LF loop reads (and would reject) the symbol at jm before
+                // the interval empties there
+                if (pv.at((uint64_t)jm) >= sigma) { lo = hi = 0; return kStatusSymbol; }
+                hi = lo;
+            } else {
+                rloc = (P)(x - idx);
+            }
             return 0;
         }
         idx -= 1;
-        const uint32_t c = s.enc[p[rev ? m - 1 - idx : idx]];
         if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
         const P plo = lo + (lo < sent ? P(1) : P(0));  // bwm/mod.rs:202-204
         const P phi = hi + (hi < sent ? P(1) : P(0));
         const P rlo = O::rank_at(a, plo, c);
         const P rhi = O::rank_at(a, phi, c);
         const P pre = s.C[c];
+        c = idx > 0 ? pv.at(idx - 1) : 0;
         lo = pre + rlo;
         hi = pre + rhi;
     }

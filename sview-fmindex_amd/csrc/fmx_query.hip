@@ -60,20 +60,58 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total,
 
 // ----------------------------------------------------------------- k_count
 
+// Stage the workgroup's patterns [first, first+256) as encoded symbols in
+// LDS (pattern order; a reversed input range is stored reversed, which puts
+// every pattern back in pattern order).  Returns false if they do not fit.
+template <typename P>
+__device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
+                                               const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
+                                               uint64_t &b0, uint64_t &b1) {
+    const uint64_t last = first + 256 < npat ? first + 256 : npat;
+    b0 = offs[first];
+    b1 = offs[last];
+    const uint64_t len = b1 - b0;
+    if (len > kStageBytes) return false;
+    for (uint64_t x = threadIdx.x; x < len; x += 256) {
+        const uint8_t v = s.enc[bytes[b0 + x]];
+        s_pat[rev ? len - 1 - x : x] = v;
+    }
+    return true;
+}
+
+template <typename P>
+__device__ __forceinline__ PatView pattern_view(const Tables<P> &s, const uint8_t *s_pat, bool staged,
+                                                const uint8_t *bytes, const uint64_t *offs, uint64_t i,
+                                                uint64_t b0, uint64_t b1, bool rev) {
+    PatView pv;
+    const uint64_t beg = offs[i], end = offs[i + 1];
+    pv.m = end - beg;
+    pv.rev = rev;
+    pv.raw = bytes + beg;
+    pv.enc = s.enc;
+    pv.sym = staged ? s_pat + (rev ? b1 - end : beg - b0) : nullptr;
+    return pv;
+}
+
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
                                                const uint64_t *__restrict__ offs, uint64_t npat,
                                                uint32_t flags, P *__restrict__ out_cnt) {
     __shared__ Tables<P> s;
+    __shared__ uint8_t s_pat[kStageBytes];
     stage_tables(a, s);
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
+    const uint64_t first = (uint64_t)blockIdx.x * 256u;
+    uint64_t b0, b1;
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, b0, b1);
+    __syncthreads();
+    const uint64_t i = first + threadIdx.x;
     if (i >= npat) return;
-    const uint64_t beg = offs[i];
+    const PatView pv = pattern_view(s, s_pat, staged, bytes, offs, i, b0, b1, rev);
     P lo, hi, rloc;
     bool res;
-    const uint32_t bad = search<P, N, VB, REC>(a, s, bytes + beg, offs[i + 1] - beg,
-                                               (flags & FMX_PATTERN_REVERSED) != 0, lo, hi, rloc, res);
+    const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, res);
     if (bad) atomicOr(a.status, bad);
     out_cnt[i] = hi - lo;
 }
@@ -91,6 +129,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
                                                 uint32_t *__restrict__ ctl, uint64_t *__restrict__ tiles,
                                                 uint32_t tiles_cap) {
     __shared__ Tables<P> s;
+    __shared__ uint8_t s_pat[kStageBytes];
     __shared__ uint64_t s_scan[4];
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_tile, s_par;
@@ -116,13 +155,16 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     for (uint64_t x = (uint64_t)g * 256 + threadIdx.x; x < tiles_cap; x += (uint64_t)G * 256) nxt[x] = 0;
 
     // ---- 1. SA interval of every pattern of the tile ----------------------
+    const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
+    uint64_t b0, b1;
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, b0, b1);
+    __syncthreads();
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     P lo = 0, hi = 0, rloc = 0;
     bool res = false;
     if (i < npat) {
-        const uint64_t beg = offs[i];
-        const uint32_t bad = search<P, N, VB, REC>(a, s, bytes + beg, offs[i + 1] - beg,
-                                                   (flags & FMX_PATTERN_REVERSED) != 0, lo, hi, rloc, res);
+        const PatView pv = pattern_view(s, s_pat, staged, bytes, offs, i, b0, b1, rev);
+        const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, res);
         if (bad) atomicOr(a.status, bad);
         if (out_cnt) out_cnt[i] = hi - lo;
     }
@@ -426,7 +468,10 @@ hipError_t build_full_sa(fmx_index *ix, hipStream_t stream) {
 
 hipError_t build_text(fmx_index *ix, hipStream_t stream) {
     const uint64_t n = ix->bv.n;
-    hipError_t e = hipMalloc(&ix->d_text, std::max<uint64_t>(n, 1));
+    // padded by 16 zero bytes: tail_mismatch reads aligned words past the end
+    hipError_t e = hipMalloc(&ix->d_text, n + 16);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(ix->d_text, 0, n + 16, stream);
     if (e != hipSuccess) return e;
     if (ix->bv.L.pos_bytes == 4)
         hipLaunchKernelGGL((k_text<uint32_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,

@@ -95,7 +95,7 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
         for (uint64_t r = 0; r < ox.n; ++r) safull[r] = walk_row<P, N, VB, REC>(a, t.C, (P)r);
         a.safull = reinterpret_cast<const uint8_t *>(safull.data());
         if (options & 8u) {
-            text.assign(ox.n, 0);
+            text.assign(ox.n + 16, 0);  // padded like the device copy
             for (uint64_t r = 0; r < ox.n; ++r) {
                 uint32_t c = 0;
                 while (c + 1 < ox.sigma && (uint64_t)t.C[c + 1] <= r) ++c;
@@ -106,11 +106,22 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
     }
     // queries (k_locate without the scan: outputs are in pattern order anyway)
     uint64_t out = 0;
+    std::vector<uint8_t> staged;
     for (uint64_t i = 0; i < npat; ++i) {
         P lo, hi, rloc;
         bool res;
-        const uint32_t bad = search<P, N, VB, REC>(a, t, bytes + offs[i], offs[i + 1] - offs[i],
-                                                   (flags & 1u) != 0, lo, hi, rloc, res);
+        PatView pv;
+        pv.m = offs[i + 1] - offs[i];
+        pv.rev = (flags & 1u) != 0;
+        pv.raw = bytes + offs[i];
+        pv.enc = t.enc;
+        pv.sym = nullptr;
+        if (i % 2 == 0) {  // odd patterns read raw bytes, even ones a staged copy (both kernel paths)
+            staged.resize(pv.m + 1);
+            for (uint64_t j = 0; j < pv.m; ++j) staged[j] = pv.at(j);
+            pv.sym = staged.data();
+        }
+        const uint32_t bad = search<P, N, VB, REC>(a, t, pv, lo, hi, rloc, res);
         if (bad) return bad == kStatusEmpty ? ORC_E_EMPTY_PATTERN : ORC_E_SYMBOL;
         const uint64_t cnt = (uint64_t)(hi - lo);
         counts[i] = cnt;

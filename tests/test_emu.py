@@ -86,3 +86,26 @@ def test_device_code_repetitive(emu, O):
             blob = O.build(text, 4, O.layout(*layout[:3]), 3, sr, table)
             for options in OPTIONS:
                 check(emu, O, blob, layout, pats, options)
+
+
+def test_device_code_text_start_and_symbols(emu, O):
+    """Tails that run into the text start, and PassThrough bytes >= sigma reached
+    (or not) by the search: per pattern, the same status as the oracle."""
+    rng = np.random.default_rng(77)
+    text = bytes([3, 2, 1, 0]) + bytes(rng.integers(0, 3, size=3000).astype(np.uint8))  # [3,2,1,0] unique start
+    for layout in [(4, 2, 64, 1), (8, 3, 32, 1)]:
+        blob = O.build(text, 4, O.layout(*layout[:3]), 2, 3, None)
+        orc = O.OracleIndex(blob, O.layout(*layout))
+        pats = [bytes([0, 3, 2, 1, 0]), bytes([1, 1, 3, 2, 1, 0, 2]), bytes([9, 3, 2, 1, 0]),
+                bytes([3, 2, 1, 0]), bytes([9, 9, 2, 2, 1]), bytes([2, 9, 0, 1, 2, 0, 1])]
+        pats += [bytes([9]) + text[s:s + 12] for s in rng.integers(4, 2900, size=40)]
+        pats += [text[s:s + 12] + bytes([7]) for s in rng.integers(4, 2900, size=10)]
+        for p in pats:
+            for options in OPTIONS:
+                try:
+                    want = ("ok", sorted(orc.locate(p)), orc.locate(p))
+                except O.OracleError as e:
+                    want = ("err", e.code)
+                st, cnt, locs = emu_locate(emu, blob, layout, options, [p])
+                got = ("ok", sorted(int(x) for x in locs), [int(x) for x in locs]) if st == 0 else ("err", st)
+                assert got == want, (p, options, got, want)
