@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+RANDOM_LINE_CEILING = 47.0  # G random 64-B line requests/s, 1-128 GB buffers, >=1M lanes (profiles/r01_randline.jsonl)
 METRIC = "patterns/sec (count+locate), 1 Gbp text / 20 bp patterns, 1/2/4/8 MI355X"
 
 ACGTN = [b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"]
@@ -78,7 +79,8 @@ def parse():
     ap.add_argument("--occ", default="interleaved", choices=["interleaved", "blob"])
     ap.add_argument("--no-deep-lut", action="store_true", help="do not build the device K-mer interval table")
     ap.add_argument("--options", type=int, default=-1,
-                    help="fmx_load options bit field (FMX_OCC_INTERLEAVED=1|DEEP_LUT=2|FULL_SA=4|TEXT=8); "
+                    help="fmx_load options bit field (FMX_OCC_INTERLEAVED=1|DEEP_LUT=2|FULL_SA=4|TEXT=8|"
+                         "ROW_CONTEXT=16); "
                          "default: everything (minus --no-deep-lut)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -234,9 +236,11 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             pm = json.load(open(args.traffic_json))
-            if key in pm.get("per_launch_bytes", {}):
-                traffic = pm["per_launch_bytes"][key]
-                traffic_src = os.path.relpath(args.traffic_json, ROOT)
+            run = pm.get("runs", {}).get(key)
+            if run and "hbm_bytes_per_launch" in run:
+                traffic = run["hbm_bytes_per_launch"]
+                traffic_src = f"{os.path.relpath(args.traffic_json, ROOT)} [{key}] (rocprofv3 FETCH_SIZE, " \
+                              f"tag {run.get('tag')}, avg {run.get('avg_duration_ns', 0) / 1e3:.1f} us/launch)"
         except Exception:
             pass
 
@@ -283,6 +287,12 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
             "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pattern": alg_bytes / B,
             "avg_launch_ms": kern.get(dominant),
+            # the binding resource of a dependent-gather kernel: 64-B HBM line
+            # requests per second vs the measured random-line ceiling
+            # (scripts/micro/randline.hip, profiles/r01_randline.jsonl)
+            "hbm_lines_per_pattern": None if traffic is None else traffic / 64 / B,
+            "hbm_glines_per_s": None if traffic is None else traffic / 64 / (kern[dominant] * 1e-3) / 1e9,
+            "random_line_ceiling_glines_per_s": RANDOM_LINE_CEILING,
         },
         "kernels_ms_per_launch": kern,
         "occurrences_per_step": total_occ,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 1u
+#define FMX_ABI_VERSION 2u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -75,7 +75,13 @@ typedef struct fmx_layout {
 #define FMX_OPT_TEXT 8u        /* the text (n symbol indices), recovered from the full SA; once an
                                   interval is a single row, the rest of the pattern is compared
                                   against the text instead of LF-stepped (needs FMX_OPT_FULL_SA) */
-#define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT)
+#define FMX_OPT_ROW_CONTEXT 16u /* full SA stored as row records {SA[r], ctx[r]} (2P per row), ctx =
+                                  the up to context_len symbols preceding the suffix, packed base
+                                  sigma+1; an interval of at most FMX_SCAN_ROWS rows (environment,
+                                  default 32) is finished by one contiguous scan of its records
+                                  instead of LF steps (implies FMX_OPT_FULL_SA | FMX_OPT_TEXT)    */
+#define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | \
+                         FMX_OPT_ROW_CONTEXT)
 
 typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
 
@@ -91,6 +97,8 @@ typedef struct fmx_index_info {
     uint32_t options;        /* FMX_OCC_* | FMX_OPT_* in effect                   */
     uint32_t deep_lut_k;     /* K of the deep k-mer table (0 = none)              */
     int32_t device;
+    uint32_t context_len;    /* symbols per row context (0 = no row records)      */
+    uint32_t scan_rows;      /* largest interval finished by a record scan        */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {

@@ -32,7 +32,8 @@ FMX_OCC_INTERLEAVED = 1
 FMX_OPT_DEEP_LUT = 2
 FMX_OPT_FULL_SA = 4
 FMX_OPT_TEXT = 8
-FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT
+FMX_OPT_ROW_CONTEXT = 16
+FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | FMX_OPT_ROW_CONTEXT
 
 
 class fmx_layout(C.Structure):
@@ -45,7 +46,8 @@ class fmx_index_info(C.Structure):
                 ("blob_len", C.c_uint64), ("device_bytes", C.c_uint64),
                 ("symbol_count", C.c_uint32), ("kmer_size", C.c_uint32),
                 ("sampling_ratio", C.c_uint32), ("block_len", C.c_uint32),
-                ("options", C.c_uint32), ("deep_lut_k", C.c_uint32), ("device", C.c_int32)]
+                ("options", C.c_uint32), ("deep_lut_k", C.c_uint32), ("device", C.c_int32),
+                ("context_len", C.c_uint32), ("scan_rows", C.c_uint32)]
 
 
 class fmx_kernel_timing(C.Structure):

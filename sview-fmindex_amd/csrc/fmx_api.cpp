@@ -270,14 +270,34 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
             ix->options |= FMX_OPT_DEEP_LUT;
         }
     }
+    if (options & FMX_OPT_ROW_CONTEXT) options |= FMX_OPT_FULL_SA | FMX_OPT_TEXT;
     if ((options & (FMX_OPT_FULL_SA | FMX_OPT_TEXT)) && v.n > 0) {
-        if (build_full_sa(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+        // row records {SA, ctx}: ctx_len = the most sigma+1-ary digits below 2^(8P)
+        uint32_t ctx_len = 0;
+        if (options & FMX_OPT_ROW_CONTEXT) {
+            const unsigned __int128 lim = (unsigned __int128)1 << (8 * v.L.pos_bytes);
+            unsigned __int128 w = 1;
+            while (ctx_len < 64 && w * (v.sigma + 1) < lim) { w *= v.sigma + 1; ++ctx_len; }
+        }
+        q.sa_stride = ctx_len ? 2 : 1;
+        if (build_full_sa(ix, q.sa_stride, ix->stream) != hipSuccess) return FMX_E_DEVICE;
         q.safull = ix->d_safull;
         ix->options |= FMX_OPT_FULL_SA;
         if (options & FMX_OPT_TEXT) {
             if (build_text(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
             q.text = ix->d_text;
             ix->options |= FMX_OPT_TEXT;
+        }
+        if (ctx_len) {
+            uint32_t scan = 32;
+            if (const char *env = getenv("FMX_SCAN_ROWS")) scan = (uint32_t)strtoul(env, nullptr, 10);
+            if (scan < 1 || scan > 64) return FMX_E_CONFIG;
+            q.ctx_len = ctx_len;
+            q.scan_rows = scan;
+            q.wpow[0] = 1;
+            for (uint32_t i = 1; i <= ctx_len; ++i) q.wpow[i] = q.wpow[i - 1] * (v.sigma + 1);
+            if (build_row_context(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+            ix->options |= FMX_OPT_ROW_CONTEXT;
         }
     }
     return FMX_OK;
@@ -421,13 +441,15 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->sentinel_index = ix->bv.sentinel;
     o->blob_len = ix->blob_len;
     o->device_bytes = (ix->d_blob_owned ? ix->blob_len : 0) + ix->occ_bytes + ix->dlut_bytes +
-                      (ix->d_safull ? ix->bv.n * ix->bv.L.pos_bytes : 0) + (ix->d_text ? ix->bv.n : 0);
+                      ix->safull_bytes + (ix->d_text ? ix->bv.n + 16 : 0);
     o->symbol_count = ix->bv.sigma;
     o->kmer_size = ix->bv.k;
     o->sampling_ratio = ix->bv.sr;
     o->block_len = ix->bv.bl;
     o->options = ix->options;
     o->deep_lut_k = ix->qa.dlut_k;
+    o->context_len = ix->qa.ctx_len;
+    o->scan_rows = ix->qa.scan_rows;
     o->device = ix->device;
     return FMX_OK;
 }

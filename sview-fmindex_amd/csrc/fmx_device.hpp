@@ -216,12 +216,13 @@ FMX_HD uint32_t load4(const uint8_t *t, uint64_t a) {
 // x - idx.  The LF loop would consume P[idx-1], P[idx-2], ... and stop at the
 // first symbol that does not precede the suffix (or at the text start); here
 // the same positions are compared with T[x-1], T[x-2], ... four at a time.
+// Only positions below `top` are compared (top = idx: all of them).
 // Returns the highest position jm that fails (-1: P occurs at x - idx).
 template <typename P>
-FMX_HD int64_t tail_mismatch(const QueryArgs &a, const PatView &pv, uint64_t idx, uint64_t x) {
+FMX_HD int64_t tail_mismatch(const QueryArgs &a, const PatView &pv, uint64_t idx, uint64_t x, uint64_t top) {
     const uint64_t lowest = idx > x ? idx - x : 0;  // positions below have no text before them
     const uint64_t tb = x - idx;                     // text position of P[0] (mod 2^64)
-    uint64_t hj = idx;
+    uint64_t hj = top;
     while (hj > lowest) {
         const uint64_t lj = hj - lowest >= 4 ? hj - 4 : lowest;
         const uint32_t tw = load4(a.text, tb + lj);
@@ -235,20 +236,74 @@ FMX_HD int64_t tail_mismatch(const QueryArgs &a, const PatView &pv, uint64_t idx
     return lowest > 0 ? (int64_t)(lowest - 1) : -1;
 }
 
+// How a search ended (what the locate phase does with an occurrence):
+constexpr uint32_t kHitRows = 0;  // rows lo..hi of the final interval: walk (or read the full SA)
+constexpr uint32_t kHitOne = 1;   // resolved: the count is hi - lo <= 1 and rloc is the location
+constexpr uint32_t kHitMask = 2;  // set bits b of `mask`: location SA[lo + b] - rloc
+
+// Row-context scan (FMX_OPT_ROW_CONTEXT).  Every row r of the interval
+// [lo, hi) of P[idx..m) starts with P[idx..m); P occurs at SA[r] - idx iff the
+// idx symbols before that suffix are P[0..idx).  The nearest ctx_len of them
+// are ctx[r] (digits sigma+1-ary, T[SA-1] most significant, 0 = before the
+// text start), so one comparison of ctx[r] against a range settles up to
+// ctx_len positions, and the rest (idx > ctx_len) is compared with the text.
+// The matching rows keep the interval's row order, which is the final
+// interval's order: all occurrences share the prefix P[0..idx), so their
+// suffixes at SA - idx sort as the suffixes at SA do.  This is the LF loop's
+// result over the same rows (with_slice.rs:27-31); callers only scan when no
+// symbol of P is >= sigma (which the LF loop would have to reject in place).
+template <typename P>
+FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo, P &hi, P &rloc, uint64_t &mask,
+                      uint32_t &mode) {
+    const uint32_t W = a.sigma + 1, Cl = a.ctx_len;
+    const uint64_t L = idx < Cl ? idx : Cl;
+    uint64_t code = 0;
+    for (uint64_t j = 0; j < L; ++j) code = code * W + (pv.at(idx - 1 - j) + 1);
+    const uint64_t span = a.wpow[Cl - L];
+    const uint64_t clo = code * span, chi = clo + span;  // ctx in [clo, chi)
+    struct alignas(2 * sizeof(P)) Rec { P sa, ctx; };
+    const Rec *rec = reinterpret_cast<const Rec *>(a.safull) + lo;
+    const uint32_t rows = (uint32_t)(hi - lo);
+    uint64_t msk = 0;
+    P first = 0;
+    for (uint32_t r = 0; r < rows; ++r) {
+        const Rec e = rec[r];
+        bool ok = (uint64_t)e.ctx >= clo && (uint64_t)e.ctx < chi;
+        if (ok && idx > Cl) ok = tail_mismatch<P>(a, pv, idx, (uint64_t)e.sa, idx - Cl) < 0;
+        if (ok) {
+            if (!msk) first = e.sa;
+            msk |= 1ull << r;
+        }
+    }
+    const uint32_t cnt = (uint32_t)__builtin_popcountll(msk);
+    if (cnt <= 1) {
+        mode = kHitOne;
+        hi = lo + (P)cnt;
+        rloc = cnt ? (P)(first - (P)idx) : P(0);
+    } else {
+        mode = kHitMask;
+        hi = lo + (P)cnt;
+        rloc = (P)idx;
+        mask = msk;
+    }
+}
+
 // k-mer seed + LF loop: FmIndex::get_pos_range (with_slice.rs:21-33).
-// Returns status bits (0 = ok).  With the recovered text, a single-row
-// interval ends the loop through tail_mismatch; `res` is then set and `rloc`
-// holds the location when the count is 1.
+// Returns status bits (0 = ok).  The result is the interval [lo, hi) with
+// mode kHitRows, or (derived structures) an interval finished early: a
+// single row checked against the text (kHitOne), or a row-context scan
+// (kHitOne / kHitMask, see scan_rows).  The count is always hi - lo.
 template <typename P, int N, int VB, int REC>
 FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv, P &lo, P &hi, P &rloc,
-                       bool &res) {
+                       uint64_t &mask, uint32_t &mode) {
     using O = Occ<P, N, VB, REC>;
     const uint32_t sigma = a.sigma, k = a.k;
     const uint64_t m = pv.m;
     const P sent = (P)a.sentinel;
     lo = hi = 0;
     rloc = 0;
-    res = false;
+    mask = 0;
+    mode = kHitRows;
     if (m == 0) return kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
     uint64_t idx;
     uint32_t bad = 0;
@@ -284,13 +339,21 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
         lo = kt[code - 1];
         hi = kt[e];
     }
+    // a PassThrough pattern with a byte >= sigma must reach it in the LF loop
+    bool scan = a.ctx_len != 0;
+    if (scan && a.strict)
+        for (uint64_t j = 0; j < idx; ++j) scan &= pv.at(j) < sigma;
     // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
     uint32_t c = idx > 0 ? pv.at(idx - 1) : 0;  // next symbol, fetched one step ahead
     while (lo < hi && idx > 0) {
+        if (scan && hi - lo <= (P)a.scan_rows) {
+            scan_rows<P>(a, pv, idx, lo, hi, rloc, mask, mode);
+            return 0;
+        }
         if (a.text != nullptr && hi - lo == P(1)) {
-            const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[lo];
-            const int64_t jm = tail_mismatch<P>(a, pv, idx, x);
-            res = true;
+            const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[(uint64_t)lo * a.sa_stride];
+            const int64_t jm = tail_mismatch<P>(a, pv, idx, x, idx);
+            mode = kHitOne;
             if (jm >= 0) {
                 // the LF loop reads (and would reject) the symbol at jm before
                 // the interval empties there
@@ -320,7 +383,7 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
 template <typename P, int N, int VB, int REC>
 FMX_HD P walk_row(const QueryArgs &a, const P *C, P pos) {
     using O = Occ<P, N, VB, REC>;
-    if (a.safull != nullptr) return reinterpret_cast<const P *>(a.safull)[pos];
+    if (a.safull != nullptr) return reinterpret_cast<const P *>(a.safull)[(uint64_t)pos * a.sa_stride];
     const P sent = (P)a.sentinel;
     P off = 0;
     uint64_t rem;

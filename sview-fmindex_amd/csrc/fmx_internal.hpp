@@ -64,8 +64,13 @@ struct QueryArgs {
     const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every sigma^dlut_k string, or null
     uint32_t dlut_k;
     uint32_t pad_;
-    const uint8_t *safull;    // full suffix array [P; n] (FMX_OPT_FULL_SA), or null
+    const uint8_t *safull;    // full suffix array: SA[r] = P at safull[r * sa_stride] (FMX_OPT_FULL_SA), or null
     const uint8_t *text;      // text as symbol indices [u8; n] (FMX_OPT_TEXT), or null
+    uint32_t sa_stride;       // 1: plain full SA; 2: row records {SA[r], ctx[r]} (FMX_OPT_ROW_CONTEXT)
+    uint32_t ctx_len;         // symbols per row context (0: no contexts)
+    uint32_t scan_rows;       // intervals of at most this many rows are finished by a record scan
+    uint32_t pad2_;
+    uint64_t wpow[65];        // (sigma+1)^i, i <= ctx_len
     uint64_t C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
     uint8_t enc[256];
@@ -103,6 +108,7 @@ struct fmx_index {
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
     uint8_t *d_safull = nullptr;
+    uint64_t safull_bytes = 0;
     uint8_t *d_text = nullptr;
     uint32_t options = 0;
     fmx::QueryArgs qa{};
@@ -135,9 +141,11 @@ hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
 // Build the deep k-mer table (FMX_OPT_DEEP_LUT) for K into ix->d_dlut.
 hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream);
 // Recover the full suffix array into ix->d_safull (FMX_OPT_FULL_SA).
-hipError_t build_full_sa(fmx_index *ix, hipStream_t stream);
+hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream);
 // Recover the text (symbol indices) into ix->d_text from d_safull (FMX_OPT_TEXT).
 hipError_t build_text(fmx_index *ix, hipStream_t stream);
+// Fill the context half of the row records (FMX_OPT_ROW_CONTEXT) from d_text.
+hipError_t build_row_context(fmx_index *ix, hipStream_t stream);
 uint32_t interleaved_record_bytes(const BlobView &bv);
 
 // GPU builder (fmx_build.hip).

@@ -110,8 +110,9 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
     if (i >= npat) return;
     const PatView pv = pattern_view(s, s_pat, staged, bytes, offs, i, b0, b1, rev);
     P lo, hi, rloc;
-    bool res;
-    const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, res);
+    uint64_t mask;
+    uint32_t mode;
+    const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
     if (bad) atomicOr(a.status, bad);
     out_cnt[i] = hi - lo;
 }
@@ -161,10 +162,11 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     __syncthreads();
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     P lo = 0, hi = 0, rloc = 0;
-    bool res = false;
+    uint64_t mask = 0;
+    uint32_t mode = kHitRows;
     if (i < npat) {
         const PatView pv = pattern_view(s, s_pat, staged, bytes, offs, i, b0, b1, rev);
-        const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, res);
+        const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
         if (bad) atomicOr(a.status, bad);
         if (out_cnt) out_cnt[i] = hi - lo;
     }
@@ -237,10 +239,21 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
         const P lo_j = __shfl(lo, jl);
         const uint64_t off_j = __shfl(my_off, jl);
         const P rloc_j = __shfl(rloc, jl);
-        const int res_j = __shfl((int)res, jl);
+        const uint32_t mode_j = (uint32_t)__shfl((int)mode, jl);
+        const uint64_t mask_j = __shfl(mask, jl);
         if (t < end) {
-            // a pattern resolved against the text already knows its one location
-            const P loc = res_j ? rloc_j : walk_row<P, N, VB, REC>(a, s.C, lo_j + (P)(t - off_j));
+            const uint64_t q = t - off_j;  // occurrence q of pattern jl
+            P loc;
+            if (mode_j == kHitOne) {
+                loc = rloc_j;  // resolved against the text: its one location
+            } else if (mode_j == kHitMask) {
+                uint64_t mk = mask_j;  // the q-th matching row of a scanned interval
+                for (uint64_t u = 0; u < q; ++u) mk &= mk - 1;
+                const P row = lo_j + (P)__builtin_ctzll(mk);
+                loc = reinterpret_cast<const P *>(a.safull)[(uint64_t)row * a.sa_stride] - rloc_j;
+            } else {
+                loc = walk_row<P, N, VB, REC>(a, s.C, lo_j + (P)q);
+            }
             if (t < cap) out_locs[t] = loc;
         }
     }
@@ -288,27 +301,43 @@ __global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *
 // SA[r] for every reduced row r: the locate walk of every row
 // (locate/mod.rs:19-35), done once at load.
 template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_full_sa(const QueryArgs a, uint64_t n, P *__restrict__ sa_out) {
+__global__ __launch_bounds__(256) void k_full_sa(const QueryArgs a, uint64_t n, P *__restrict__ sa_out,
+                                                 uint32_t stride) {
     __shared__ Tables<P> s;
     stage_tables(a, s);
     __syncthreads();
     QueryArgs b = a;
     b.safull = nullptr;
     for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256)
-        sa_out[r] = walk_row<P, N, VB, REC>(b, s.C, (P)r);
+        sa_out[r * stride] = walk_row<P, N, VB, REC>(b, s.C, (P)r);
 }
 
 // T[SA[r]] = first symbol of row r's suffix = the c with C[c] <= r < C[c+1].
 template <typename P>
 __global__ __launch_bounds__(256) void k_text(const QueryArgs a, uint64_t n, const P *__restrict__ sa,
-                                              uint8_t *__restrict__ text) {
+                                              uint32_t stride, uint8_t *__restrict__ text) {
     __shared__ P sC[kMaxSigma + 1];
     if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
     __syncthreads();
     for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256) {
         uint32_t c = 0;
         while (c + 1 < a.sigma && (uint64_t)sC[c + 1] <= r) ++c;
-        text[(uint64_t)sa[r]] = (uint8_t)c;
+        text[(uint64_t)sa[r * stride]] = (uint8_t)c;
+    }
+}
+
+// Row contexts (FMX_OPT_ROW_CONTEXT): rec[2r+1] = T[x-1], T[x-2], ..., T[x-ctx_len]
+// (x = SA[r] = rec[2r]) as sigma+1-ary digits, symbol + 1, 0 before the text
+// start, the nearest symbol most significant.
+template <typename P>
+__global__ __launch_bounds__(256) void k_row_ctx(const QueryArgs a, uint64_t n, const uint8_t *__restrict__ text,
+                                                 P *__restrict__ rec) {
+    const uint32_t W = a.sigma + 1, Cl = a.ctx_len;
+    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256) {
+        const uint64_t x = (uint64_t)rec[2 * r];
+        uint64_t v = 0;
+        for (uint32_t j = 1; j <= Cl; ++j) v = v * W + (j <= x ? (uint64_t)text[x - j] + 1 : 0);
+        rec[2 * r + 1] = (P)v;
     }
 }
 
@@ -453,13 +482,14 @@ static inline unsigned grid_stride_for(uint64_t n) {
     return (unsigned)(g < 65536 ? (g ? g : 1) : 65536);
 }
 
-hipError_t build_full_sa(fmx_index *ix, hipStream_t stream) {
+hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream) {
     const uint64_t n = ix->bv.n;
-    hipError_t e = hipMalloc(&ix->d_safull, std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes);
+    hipError_t e = hipMalloc(&ix->d_safull, std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes * stride);
     if (e != hipSuccess) return e;
+    ix->safull_bytes = std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes * stride;
     e = dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         hipLaunchKernelGGL((k_full_sa<P, N, VB, R>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
-                           (P *)ix->d_safull);
+                           (P *)ix->d_safull, stride);
         return hipGetLastError();
     });
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
@@ -473,13 +503,27 @@ hipError_t build_text(fmx_index *ix, hipStream_t stream) {
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(ix->d_text, 0, n + 16, stream);
     if (e != hipSuccess) return e;
+    const uint32_t stride = ix->qa.sa_stride;
     if (ix->bv.L.pos_bytes == 4)
         hipLaunchKernelGGL((k_text<uint32_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
-                           (const uint32_t *)ix->d_safull, ix->d_text);
+                           (const uint32_t *)ix->d_safull, stride, ix->d_text);
     else
         hipLaunchKernelGGL((k_text<uint64_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
-                           (const uint64_t *)ix->d_safull, ix->d_text);
+                           (const uint64_t *)ix->d_safull, stride, ix->d_text);
     e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e;
+}
+
+hipError_t build_row_context(fmx_index *ix, hipStream_t stream) {
+    const uint64_t n = ix->bv.n;
+    if (ix->bv.L.pos_bytes == 4)
+        hipLaunchKernelGGL((k_row_ctx<uint32_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
+                           ix->d_text, (uint32_t *)ix->d_safull);
+    else
+        hipLaunchKernelGGL((k_row_ctx<uint64_t>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
+                           ix->d_text, (uint64_t *)ix->d_safull);
+    hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     return e;
 }

@@ -21,6 +21,8 @@ namespace {
 template <typename P, int N, int VB, int REC>
 int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
         uint32_t flags, uint64_t *counts, uint64_t *locs, uint64_t cap, uint64_t *needed) {
+    const uint32_t scan_rows = options >> 8 ? options >> 8 : 32;  // options bits 8..: FMX_SCAN_ROWS
+    options &= 0xffu;
     QueryArgs a{};
     const uint8_t *blob = ox.blob;
     a.ckpt = blob + ox.off_ckpt;
@@ -87,21 +89,42 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
             a.dlut_k = K;
         }
     }
-    // full SA (k_full_sa) and text (k_text)
+    // full SA (k_full_sa), text (k_text), row contexts (k_row_ctx)
     std::vector<P> safull;
     std::vector<uint8_t> text;
+    if (options & 16u) options |= 4u | 8u;
     if ((options & (4u | 8u)) && ox.n > 0) {
-        safull.resize(ox.n);
-        for (uint64_t r = 0; r < ox.n; ++r) safull[r] = walk_row<P, N, VB, REC>(a, t.C, (P)r);
+        uint32_t ctx_len = 0;
+        if (options & 16u) {
+            const unsigned __int128 lim = (unsigned __int128)1 << (8 * sizeof(P));
+            unsigned __int128 w = 1;
+            while (ctx_len < 64 && w * (ox.sigma + 1) < lim) { w *= ox.sigma + 1; ++ctx_len; }
+        }
+        const uint32_t stride = ctx_len ? 2 : 1;
+        a.sa_stride = stride;
+        safull.resize(ox.n * stride);
+        for (uint64_t r = 0; r < ox.n; ++r) safull[r * stride] = walk_row<P, N, VB, REC>(a, t.C, (P)r);
         a.safull = reinterpret_cast<const uint8_t *>(safull.data());
         if (options & 8u) {
             text.assign(ox.n + 16, 0);  // padded like the device copy
             for (uint64_t r = 0; r < ox.n; ++r) {
                 uint32_t c = 0;
                 while (c + 1 < ox.sigma && (uint64_t)t.C[c + 1] <= r) ++c;
-                text[(uint64_t)safull[r]] = (uint8_t)c;
+                text[(uint64_t)safull[r * stride]] = (uint8_t)c;
             }
             a.text = text.data();
+        }
+        if (ctx_len) {
+            a.ctx_len = ctx_len;
+            a.scan_rows = scan_rows;
+            a.wpow[0] = 1;
+            for (uint32_t i = 1; i <= ctx_len; ++i) a.wpow[i] = a.wpow[i - 1] * (ox.sigma + 1);
+            for (uint64_t r = 0; r < ox.n; ++r) {
+                const uint64_t x = (uint64_t)safull[2 * r];
+                uint64_t v = 0;
+                for (uint32_t j = 1; j <= ctx_len; ++j) v = v * (ox.sigma + 1) + (j <= x ? text[x - j] + 1ull : 0);
+                safull[2 * r + 1] = (P)v;
+            }
         }
     }
     // queries (k_locate without the scan: outputs are in pattern order anyway)
@@ -109,7 +132,8 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
     std::vector<uint8_t> staged;
     for (uint64_t i = 0; i < npat; ++i) {
         P lo, hi, rloc;
-        bool res;
+        uint64_t mask;
+        uint32_t mode;
         PatView pv;
         pv.m = offs[i + 1] - offs[i];
         pv.rev = (flags & 1u) != 0;
@@ -121,12 +145,22 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
             for (uint64_t j = 0; j < pv.m; ++j) staged[j] = pv.at(j);
             pv.sym = staged.data();
         }
-        const uint32_t bad = search<P, N, VB, REC>(a, t, pv, lo, hi, rloc, res);
+        const uint32_t bad = search<P, N, VB, REC>(a, t, pv, lo, hi, rloc, mask, mode);
         if (bad) return bad == kStatusEmpty ? ORC_E_EMPTY_PATTERN : ORC_E_SYMBOL;
         const uint64_t cnt = (uint64_t)(hi - lo);
         counts[i] = cnt;
         for (uint64_t j = 0; j < cnt; ++j, ++out) {
-            const P loc = res ? rloc : walk_row<P, N, VB, REC>(a, t.C, lo + (P)j);
+            P loc;
+            if (mode == kHitOne) {
+                loc = rloc;
+            } else if (mode == kHitMask) {  // the k_locate locate phase
+                uint64_t mk = mask;
+                for (uint64_t u = 0; u < j; ++u) mk &= mk - 1;
+                const P row = lo + (P)__builtin_ctzll(mk);
+                loc = safull[(uint64_t)row * a.sa_stride] - rloc;
+            } else {
+                loc = walk_row<P, N, VB, REC>(a, t.C, lo + (P)j);
+            }
             if (out < cap) locs[out] = (uint64_t)loc;
         }
     }
@@ -172,7 +206,8 @@ int by_n(const orc_index &ox, uint32_t rec, uint32_t options, const uint8_t *b, 
 
 extern "C" {
 
-// options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text).
+// options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text,
+// 16 row contexts); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
 // Outputs are u64: counts[npat] and the concatenated locations.
 int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
                uint32_t encoder, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,

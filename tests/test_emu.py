@@ -15,7 +15,9 @@ from _util import ALL_LAYOUTS, rand_chr_list, rand_pattern, rand_text, table_fro
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 EMU = os.path.join(HERE, "emu", "libfmx_emu.so")
-OPTIONS = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 2 | 8)
+# fmx_load option bits; bits 8.. set the row-scan limit (FMX_SCAN_ROWS)
+OPTIONS = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 2 | 8, 31, 16, 1 | 16 | (1 << 8), 2 | 16 | (64 << 8),
+           1 | 2 | 16 | (5 << 8))
 
 
 @pytest.fixture(scope="module")

@@ -14,9 +14,10 @@ from _util import (ALL_LAYOUTS, encode, occurrences, rand_chr_list, rand_pattern
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 # load options (FMX_OCC_INTERLEAVED=1 | FMX_OPT_DEEP_LUT=2 | FMX_OPT_FULL_SA=4 |
-# FMX_OPT_TEXT=8): the faithful blob path, each derived structure, everything;
-# a 1 MB table budget makes K > k even on the small test texts (K = 8 for sigma = 4)
-OCC_MODES = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8)
+# FMX_OPT_TEXT=8 | FMX_OPT_ROW_CONTEXT=16): the faithful blob path, each derived
+# structure, everything; a 1 MB table budget makes K > k even on the small test
+# texts (K = 8 for sigma = 4)
+OCC_MODES = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 16, 31)
 os.environ.setdefault("FMX_DEEP_LUT_MB", "1")
 
 
@@ -298,3 +299,45 @@ def test_deep_lut_info(pkg, O):
     ix.close()
     for occ in (1 | 2, 2, 1 | 2 | 4 | 8):
         check_parity(pkg, O, blob, 4, 3, 64, 0, pats, occ)
+
+
+@pytest.mark.parametrize("scan", ["1", "7", "64"])
+def test_row_context_scan_limits(pkg, O, scan, monkeypatch):
+    """FMX_OPT_ROW_CONTEXT with every scan limit (1: single rows only, 64: the
+    mask width): contexts shorter than the remaining pattern (sigma = 16 packs
+    3 symbols per u32 context... 7), repetitive text (intervals of many rows),
+    PassThrough bytes >= sigma (the scan must yield to the LF loop)."""
+    monkeypatch.setenv("FMX_SCAN_ROWS", scan)
+    rng = np.random.default_rng(int(scan))
+    for sigma, pb, planes, vb in [(16, 4, 4, 64), (4, 8, 2, 128), (5, 4, 3, 32)]:
+        chars = rand_chr_list(rng, sigma)
+        table = table_from_symbols([bytes([c]) for c in chars])
+        text = (rand_text(rng, chars, 3000, 6000) + chars[:2] * 300
+                + rand_text(rng, chars, 1000, 2000))
+        blob = gpu_build(pkg, text, sigma, pb, planes, vb, 3, 3, table)
+        pats = [rand_pattern(rng, text, 1, 40) for _ in range(1500)] + [chars[:2] * 5, chars[:2] * 40]
+        for occ in (16, 31):
+            check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+        ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=31)
+        info = ix.info()
+        assert info["scan_rows"] == int(scan) and info["context_len"] > 0
+        ix.close()
+    # PassThrough: bytes >= sigma anywhere in the pattern
+    text = bytes(rng.integers(0, 4, size=5000).astype(np.uint8))
+    blob = gpu_build(pkg, text, 4, 4, 2, 64, 2, 2, None)
+    pats = [text[s:s + 20] for s in rng.integers(0, 4900, size=300)]
+    pats += [bytes([9]) + p[1:] for p in pats[:50]] + [p[:10] + bytes([7]) + p[11:] for p in pats[50:100]]
+    orc = O.OracleIndex(blob, O.layout(4, 2, 64, 1))
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64), pkg.text_encoders.PassThrough,
+                          options=31)
+    for p in pats:
+        try:
+            want = ("ok", orc.locate(p))
+        except O.OracleError as e:
+            want = ("err", e.code)
+        try:
+            got = ("ok", [int(x) for x in ix.locate(p)])
+        except pkg.FmxError as e:
+            got = ("err", e.code)
+        assert got == want, (p, got, want)
+    ix.close()
