@@ -261,19 +261,53 @@ FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo
     for (uint64_t j = 0; j < L; ++j) code = code * W + (pv.at(idx - 1 - j) + 1);
     const uint64_t span = a.wpow[Cl - L];
     const uint64_t clo = code * span, chi = clo + span;  // ctx in [clo, chi)
-    struct alignas(2 * sizeof(P)) Rec { P sa, ctx; };
-    const Rec *rec = reinterpret_cast<const Rec *>(a.safull) + lo;
-    const uint32_t rows = (uint32_t)(hi - lo);
+    // Records are read as 16-B vectors, NV of them issued before any is used
+    // (one round covers 8 u32 / 4 u64 rows; the row-record buffer is padded so
+    // the last vector never leaves it).  Bits of msk are rows relative to lo.
+    using V4 = uint32_t __attribute__((ext_vector_type(4)));
+    constexpr uint32_t RPV = 16 / (2 * sizeof(P));
+    constexpr uint32_t NV = 4;
+    const V4 *vec = reinterpret_cast<const V4 *>(a.safull);
+    const uint64_t v0 = (uint64_t)lo / RPV, v1 = ((uint64_t)hi + RPV - 1) / RPV;
     uint64_t msk = 0;
     P first = 0;
-    for (uint32_t r = 0; r < rows; ++r) {
-        const Rec e = rec[r];
-        bool ok = (uint64_t)e.ctx >= clo && (uint64_t)e.ctx < chi;
-        if (ok && idx > Cl) ok = tail_mismatch<P>(a, pv, idx, (uint64_t)e.sa, idx - Cl) < 0;
-        if (ok) {
-            if (!msk) first = e.sa;
-            msk |= 1ull << r;
+    for (uint64_t vb = v0; vb < v1; vb += NV) {
+        V4 x[NV];
+#pragma unroll
+        for (uint32_t u = 0; u < NV; ++u) x[u] = vec[vb + u < v1 ? vb + u : v1 - 1];
+#pragma unroll
+        for (uint32_t u = 0; u < NV; ++u) {
+#pragma unroll
+            for (uint32_t w = 0; w < RPV; ++w) {
+                const uint64_t row = (vb + u) * RPV + w;
+                P sa, ctx;
+                if constexpr (sizeof(P) == 4) {
+                    sa = (P)x[u][2 * w];
+                    ctx = (P)x[u][2 * w + 1];
+                } else {
+                    sa = (P)((uint64_t)x[u][0] | (uint64_t)x[u][1] << 32);
+                    ctx = (P)((uint64_t)x[u][2] | (uint64_t)x[u][3] << 32);
+                }
+                if (row >= (uint64_t)lo && row < (uint64_t)hi && (uint64_t)ctx >= clo && (uint64_t)ctx < chi) {
+                    if (!msk) first = sa;
+                    msk |= 1ull << (row - (uint64_t)lo);
+                }
+            }
         }
+    }
+    if (idx > Cl && msk) {
+        // the symbols beyond the context: compare with the text, row by row
+        const P *sa = reinterpret_cast<const P *>(a.safull);
+        uint64_t keep = 0;
+        for (uint64_t m2 = msk; m2; m2 &= m2 - 1) {
+            const uint64_t b = (uint64_t)__builtin_ctzll(m2);
+            const P x = sa[2 * ((uint64_t)lo + b)];
+            if (tail_mismatch<P>(a, pv, idx, (uint64_t)x, idx - Cl) < 0) {
+                if (!keep) first = x;
+                keep |= 1ull << b;
+            }
+        }
+        msk = keep;
     }
     const uint32_t cnt = (uint32_t)__builtin_popcountll(msk);
     if (cnt <= 1) {

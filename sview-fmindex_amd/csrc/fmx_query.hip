@@ -484,9 +484,12 @@ static inline unsigned grid_stride_for(uint64_t n) {
 
 hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream) {
     const uint64_t n = ix->bv.n;
-    hipError_t e = hipMalloc(&ix->d_safull, std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes * stride);
+    // padded: scan_rows reads whole 16-B vectors of row records
+    ix->safull_bytes = std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes * stride + 64;
+    hipError_t e = hipMalloc(&ix->d_safull, ix->safull_bytes);
     if (e != hipSuccess) return e;
-    ix->safull_bytes = std::max<uint64_t>(n, 1) * ix->bv.L.pos_bytes * stride;
+    e = hipMemsetAsync(ix->d_safull, 0, ix->safull_bytes, stream);
+    if (e != hipSuccess) return e;
     e = dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         hipLaunchKernelGGL((k_full_sa<P, N, VB, R>), dim3(grid_stride_for(n)), dim3(256), 0, stream, ix->qa, n,
                            (P *)ix->d_safull, stride);

@@ -90,7 +90,8 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
         }
     }
     // full SA (k_full_sa), text (k_text), row contexts (k_row_ctx)
-    std::vector<P> safull;
+    std::vector<unsigned __int128> safull_store;  // 16-B aligned, padded like the device buffer
+    P *safull = nullptr;
     std::vector<uint8_t> text;
     if (options & 16u) options |= 4u | 8u;
     if ((options & (4u | 8u)) && ox.n > 0) {
@@ -102,9 +103,10 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
         }
         const uint32_t stride = ctx_len ? 2 : 1;
         a.sa_stride = stride;
-        safull.resize(ox.n * stride);
+        safull_store.assign((ox.n * stride * sizeof(P) + 64) / 16 + 1, 0);
+        safull = reinterpret_cast<P *>(safull_store.data());
         for (uint64_t r = 0; r < ox.n; ++r) safull[r * stride] = walk_row<P, N, VB, REC>(a, t.C, (P)r);
-        a.safull = reinterpret_cast<const uint8_t *>(safull.data());
+        a.safull = reinterpret_cast<const uint8_t *>(safull);
         if (options & 8u) {
             text.assign(ox.n + 16, 0);  // padded like the device copy
             for (uint64_t r = 0; r < ox.n; ++r) {
