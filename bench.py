@@ -177,7 +177,7 @@ def main():
 
     def step():
         ix.locate_batch_async(d_pat.data_ptr(), d_off.data_ptr(), B, d_loff.data_ptr(), d_locs.data_ptr(), cap,
-                              d_need.data_ptr(), d_ws.data_ptr(), ws)
+                              d_need.data_ptr(), d_ws.data_ptr(), ws, long_patterns=m > 64)
 
     for _ in range(args.warmup):
         step()

@@ -60,6 +60,9 @@ typedef struct fmx_layout {
 /* Query flags */
 #define FMX_PATTERN_REVERSED 1u /* patterns are given last byte first: the *_rev_iter forms
                                    (src/locate/with_rev_iter.rs:5-38)                          */
+#define FMX_HINT_LONG_PATTERNS 2u /* performance hint: patterns average more than 64 bytes; the
+                                   kernels stage each workgroup's patterns in 56 KB of LDS
+                                   instead of 16 KB (set automatically by the host-buffer calls) */
 
 /* Load options: device-side structures derived from the blob at load time.
  * Results are identical with any combination; they trade HBM for fewer

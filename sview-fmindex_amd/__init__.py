@@ -492,8 +492,8 @@ class FmIndex:
 
     # -- device-resident API (pointers are ints; stream is a hipStream_t) --
     def count_batch_async(self, d_bytes: int, d_offsets: int, n: int, d_counts: int,
-                          stream: int = 0, reversed: bool = False) -> None:
-        flags = _n.FMX_PATTERN_REVERSED if reversed else 0
+                          stream: int = 0, reversed: bool = False, long_patterns: bool = False) -> None:
+        flags = (_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
         _check(_n.lib().fmx_count_batch_async(self._h, C.c_void_p(d_bytes), C.c_void_p(d_offsets), n, flags,
                                               C.c_void_p(d_counts), C.c_void_p(stream) if stream else None))
 
@@ -504,8 +504,10 @@ class FmIndex:
 
     def locate_batch_async(self, d_bytes: int, d_offsets: int, n: int, d_loc_offsets: int,
                            d_locs: int, cap: int, d_needed: int, d_ws: int, ws_bytes: int,
-                           d_counts: int = 0, stream: int = 0, reversed: bool = False) -> None:
-        flags = _n.FMX_PATTERN_REVERSED if reversed else 0
+                           d_counts: int = 0, stream: int = 0, reversed: bool = False,
+                           long_patterns: bool = False) -> None:
+        """`long_patterns`: FMX_HINT_LONG_PATTERNS (patterns average > 64 bytes)."""
+        flags = (_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
         _check(_n.lib().fmx_locate_batch_async(
             self._h, C.c_void_p(d_bytes), C.c_void_p(d_offsets), n, flags,
             C.c_void_p(d_counts) if d_counts else None, C.c_void_p(d_loc_offsets), C.c_void_p(d_locs), cap,

@@ -27,6 +27,7 @@ FMX_E_CONFIG = 10
 FMX_ENC_TABLE = 0
 FMX_ENC_PASS = 1
 FMX_PATTERN_REVERSED = 1
+FMX_HINT_LONG_PATTERNS = 2
 FMX_OCC_BLOB = 0
 FMX_OCC_INTERLEAVED = 1
 FMX_OPT_DEEP_LUT = 2

@@ -527,6 +527,7 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return FMX_E_DEVICE;
+    if (nb > 64 * n) flags |= FMX_HINT_LONG_PATTERNS;
     st = fmx_count_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, d + o_cnt, s);
     if (st) return st;
     if (hipMemcpyAsync(out_counts, d + o_cnt, n * pb, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
@@ -558,6 +559,7 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
     if (st) return st;
     hipSetDevice(ix->device);
     const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
+    if (nb > 64 * n) flags |= FMX_HINT_LONG_PATTERNS;
     st = ensure_ws(ix, n);
     if (st) return st;
     const uint64_t o_off = align_up(nb, 256);

@@ -16,7 +16,8 @@ namespace fmx {
 
 constexpr int kMaxSigma = 64;  // Block6 indexes at most 2^6 symbols (blocks/block6.rs:15)
 constexpr int kMaxK = 40;      // W^k must fit the u32 header field anyway (count_array.rs:68)
-constexpr int kStageBytes = 16384;  // LDS bytes for a workgroup's 256 patterns (else read from HBM)
+constexpr int kStageBytes = 16384;      // LDS bytes for a workgroup's 256 patterns (else read from HBM)
+constexpr int kStageBytesLong = 57344;  // the same with FMX_HINT_LONG_PATTERNS
 
 // Parsed blob headers.  Field-for-field what FmIndex::load derives
 // (src/load_from_blob.rs:28-85); offsets are byte offsets into the blob.

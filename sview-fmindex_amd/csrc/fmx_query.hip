@@ -66,12 +66,12 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total,
 template <typename P>
 __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
                                                const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
-                                               uint64_t &b0, uint64_t &b1) {
+                                               uint32_t stage_bytes, uint64_t &b0, uint64_t &b1) {
     const uint64_t last = first + 256 < npat ? first + 256 : npat;
     b0 = offs[first];
     b1 = offs[last];
     const uint64_t len = b1 - b0;
-    if (len > kStageBytes) return false;
+    if (len > stage_bytes) return false;
     for (uint64_t x = threadIdx.x; x < len; x += 256) {
         const uint8_t v = s.enc[bytes[b0 + x]];
         s_pat[rev ? len - 1 - x : x] = v;
@@ -96,15 +96,15 @@ __device__ __forceinline__ PatView pattern_view(const Tables<P> &s, const uint8_
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
                                                const uint64_t *__restrict__ offs, uint64_t npat,
-                                               uint32_t flags, P *__restrict__ out_cnt) {
+                                               uint32_t flags, P *__restrict__ out_cnt, uint32_t stage_bytes) {
     __shared__ Tables<P> s;
-    __shared__ uint8_t s_pat[kStageBytes];
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     stage_tables(a, s);
     __syncthreads();
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
     const uint64_t first = (uint64_t)blockIdx.x * 256u;
     uint64_t b0, b1;
-    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, b0, b1);
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, b0, b1);
     __syncthreads();
     const uint64_t i = first + threadIdx.x;
     if (i >= npat) return;
@@ -128,9 +128,9 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
                                                 P *__restrict__ out_cnt, uint64_t *__restrict__ loc_off,
                                                 P *__restrict__ out_locs, uint64_t cap, uint64_t *__restrict__ needed,
                                                 uint32_t *__restrict__ ctl, uint64_t *__restrict__ tiles,
-                                                uint32_t tiles_cap) {
+                                                uint32_t tiles_cap, uint32_t stage_bytes) {
     __shared__ Tables<P> s;
-    __shared__ uint8_t s_pat[kStageBytes];
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     __shared__ uint64_t s_scan[4];
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_tile, s_par;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     // ---- 1. SA interval of every pattern of the tile ----------------------
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
     uint64_t b0, b1;
-    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, b0, b1);
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, b0, b1);
     __syncthreads();
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     P lo = 0, hi = 0, rloc = 0;
@@ -421,12 +421,17 @@ static inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads +
 // look-back tiles needed for n patterns (one per 256-pattern workgroup)
 uint64_t locate_tiles_cap(uint64_t n) { return (n + 255) / 256 > 0 ? (n + 255) / 256 : 1; }
 
+static inline uint32_t stage_bytes_for(uint32_t flags) {
+    return (flags & FMX_HINT_LONG_PATTERNS) ? (uint32_t)kStageBytesLong : (uint32_t)kStageBytes;
+}
+
 hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                         uint32_t flags, void *d_counts, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
-        hipLaunchKernelGGL((k_count<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, d_bytes,
-                           d_offsets, n, flags, (P *)d_counts);
+        const uint32_t sb = stage_bytes_for(flags);
+        hipLaunchKernelGGL((k_count<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
+                           d_offsets, n, flags, (P *)d_counts, sb);
         return hipGetLastError();
     });
 }
@@ -438,9 +443,10 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
     if (n == 0) return hipSuccess;
     if ((n + 255) / 256 > tiles_cap || tiles_cap > 0xFFFFFFFFull) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
-        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, d_bytes,
+        const uint32_t sb = stage_bytes_for(flags);
+        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
                            d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed, d_ctl,
-                           d_tiles, (uint32_t)tiles_cap);
+                           d_tiles, (uint32_t)tiles_cap, sb);
         return hipGetLastError();
     });
 }
