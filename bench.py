@@ -65,6 +65,31 @@ CONFIGS = {
 }
 
 
+def phase_stamps(pkg, ix, step, B, out_path):
+    """Diagnostic (FMX_LIB=.../libfmx_stamps.so): per-wave phase timestamps of
+    one k_locate launch, summarised as percentiles (10 ns ticks -> us)."""
+    import ctypes
+    L = pkg._native.lib()
+    step()
+    ix.sync()
+    waves = (B + 255) // 256 * 4
+    buf = np.zeros(waves * 8, np.uint64)
+    L.fmx_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    assert L.fmx_debug_stamps(buf.ctypes.data, buf.size) == 0
+    t = buf.reshape(waves, 8).astype(np.float64)
+    live = np.arange(waves) * 64 < B
+    t = t[live]
+    t0 = t[:, 0].min()
+    rel = (t[:, :5] - t0) / 100.0  # us
+    pct = lambda x: {q: round(float(np.percentile(x, q)), 2) for q in (0, 10, 50, 90, 100)}
+    res = {"waves": int(live.sum()), "entry": pct(rel[:, 0]), "staged": pct(rel[:, 1]), "searched": pct(rel[:, 2]),
+           "offsets": pct(rel[:, 3]), "done": pct(rel[:, 4]),
+           "stage_us": pct(rel[:, 1] - rel[:, 0]), "search_us": pct(rel[:, 2] - rel[:, 1]),
+           "lookback_us": pct(rel[:, 3] - rel[:, 2]), "locate_us": pct(rel[:, 4] - rel[:, 3])}
+    json.dump(res, open(out_path, "w"), indent=1)
+    log("[stamps] " + json.dumps(res))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,6 +229,9 @@ def main():
     timing = ix.timing_read()
     if world > 1:
         elapsed = D.max_over_ranks(elapsed, device=dev)
+
+    if os.environ.get("FMX_STAMPS_OUT"):
+        phase_stamps(pkg, ix, step, B, os.environ["FMX_STAMPS_OUT"])
 
     # ---- result concatenation across ranks (RCCL all-gathers, untimed) -----
     gather_ms = None

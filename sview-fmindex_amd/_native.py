@@ -103,7 +103,7 @@ def lib():
                 import torch  # noqa: F401
             except ImportError:
                 pass
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(os.environ.get("FMX_LIB", LIB_PATH))  # FMX_LIB: a diagnostic build (csrc `make stamps`)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)
             f.restype = res

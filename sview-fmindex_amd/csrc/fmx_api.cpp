@@ -350,7 +350,7 @@ int fmx_device_count(void) {
     return n;
 }
 
-fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, int device, uint32_t occ_mode,
+fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, int device, uint32_t options,
                     fmx_index **out, uint64_t *expected_total, uint64_t *actual_total) {
     if (!out || (!blob && blob_len)) return FMX_E_ARG;
     *out = nullptr;
@@ -377,14 +377,14 @@ fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, i
         return FMX_E_DEVICE;
     }
     ix->d_blob = ix->d_blob_owned;
-    st = finish_load(ix, occ_mode);
+    st = finish_load(ix, options);
     if (st) { fmx_free(ix); return st; }
     *out = ix;
     return FMX_OK;
 }
 
 fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout layout, int device,
-                           uint32_t occ_mode, fmx_index **out, uint64_t *expected_total, uint64_t *actual_total) {
+                           uint32_t options, fmx_index **out, uint64_t *expected_total, uint64_t *actual_total) {
     if (!out || !d_blob) return FMX_E_ARG;
     *out = nullptr;
     if (!layout_valid(layout)) return FMX_E_LAYOUT;
@@ -403,7 +403,7 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
     ix->device = device;
     ix->blob_len = blob_len;
     ix->d_blob = d_blob;
-    st = finish_load(ix, occ_mode);
+    st = finish_load(ix, options);
     if (st) { fmx_free(ix); return st; }
     *out = ix;
     return FMX_OK;

@@ -28,6 +28,21 @@
 
 namespace fmx {
 
+#ifdef FMX_PHASE_STAMPS
+// Diagnostic build only: s_memrealtime (100 MHz) per wave at each phase of
+// k_locate: [0] entry, [1] patterns staged, [2] search done, [3] offsets
+// known (look-back done), [4] locations written, [5] tile id.
+constexpr uint32_t kStampWaves = 1u << 17, kStampSlots = 8;
+__device__ uint64_t g_stamps[kStampWaves * kStampSlots];
+#define FMX_STAMP(slot, v)                                                                   \
+    do {                                                                                     \
+        const uint32_t wv_ = blockIdx.x * 4u + (threadIdx.x >> 6);                           \
+        if ((threadIdx.x & 63) == 0 && wv_ < kStampWaves) g_stamps[wv_ * kStampSlots + (slot)] = (v); \
+    } while (0)
+#else
+#define FMX_STAMP(slot, v) do { } while (0)
+#endif
+
 template <typename P>
 __device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s) {
     const int t = threadIdx.x;
@@ -134,6 +149,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     __shared__ uint64_t s_scan[4];
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_tile, s_par;
+    FMX_STAMP(0, __builtin_amdgcn_s_memrealtime());
     stage_tables(a, s);
     const uint32_t G = (uint32_t)((npat + 255) / 256);
     if (threadIdx.x == 0) {
@@ -160,6 +176,8 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     uint64_t b0, b1;
     const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, b0, b1);
     __syncthreads();
+    FMX_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    FMX_STAMP(5, g);
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     P lo = 0, hi = 0, rloc = 0;
     uint64_t mask = 0;
@@ -171,6 +189,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
         if (out_cnt) out_cnt[i] = hi - lo;
     }
     const uint64_t cnt = (uint64_t)(hi - lo);
+    FMX_STAMP(2, __builtin_amdgcn_s_memrealtime());
 
     // ---- 2. output offsets: single-pass scan with decoupled look-back -----
     uint64_t agg;
@@ -217,6 +236,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
         }
     }
     __syncthreads();
+    FMX_STAMP(3, __builtin_amdgcn_s_memrealtime());
     const uint64_t my_off = s_prefix + excl;
     if (i < npat) loc_off[i] = my_off;
     if (g == G - 1 && threadIdx.x == 0) {
@@ -257,6 +277,10 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
             if (t < cap) out_locs[t] = loc;
         }
     }
+#ifdef FMX_PHASE_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    FMX_STAMP(4, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------ deep k-mer table
@@ -551,3 +575,10 @@ hipError_t launch_relayout(fmx_index *ix, hipStream_t stream) {
 }
 
 }  // namespace fmx
+
+#ifdef FMX_PHASE_STAMPS
+extern "C" int fmx_debug_stamps(uint64_t *out, uint64_t n) {
+    if (n > (uint64_t)fmx::kStampWaves * fmx::kStampSlots) n = (uint64_t)fmx::kStampWaves * fmx::kStampSlots;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fmx::g_stamps), n * 8) == hipSuccess ? 0 : 8;
+}
+#endif
