@@ -77,29 +77,57 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total,
 
 // Stage the workgroup's patterns [first, first+256) as encoded symbols in
 // LDS (pattern order; a reversed input range is stored reversed, which puts
-// every pattern back in pattern order).  Returns false if they do not fit.
+// every pattern back in pattern order).  One round trip for the offsets (each
+// thread its own pattern's bounds, plus the tile's), one for the bytes: 16-B
+// aligned vectors, up to four per thread in flight (an aligned vector holding
+// at least one byte of the batch never leaves the batch's page).  Returns
+// false if the tile does not fit; the patterns are then read from HBM.
 template <typename P>
 __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
                                                const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
-                                               uint32_t stage_bytes, uint64_t &b0, uint64_t &b1) {
+                                               uint32_t stage_bytes, uint64_t &beg, uint64_t &end, uint64_t &b0,
+                                               uint64_t &b1) {
     const uint64_t last = first + 256 < npat ? first + 256 : npat;
+    const uint64_t i = first + threadIdx.x;
     b0 = offs[first];
     b1 = offs[last];
+    beg = i < npat ? offs[i] : 0;
+    end = i < npat ? offs[i + 1] : 0;
     const uint64_t len = b1 - b0;
     if (len > stage_bytes) return false;
-    for (uint64_t x = threadIdx.x; x < len; x += 256) {
-        const uint8_t v = s.enc[bytes[b0 + x]];
-        s_pat[rev ? len - 1 - x : x] = v;
+    using V4 = uint32_t __attribute__((ext_vector_type(4)));
+    const uint64_t a0 = b0 & ~15ull;
+    const uint32_t nv = (uint32_t)((b1 - a0 + 15) >> 4);
+    const V4 *src = reinterpret_cast<const V4 *>(bytes + a0);
+    for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 256) {
+        V4 x[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t v = v0 + u * 256 + threadIdx.x;
+            if (v < nv) x[u] = src[v];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t v = v0 + u * 256 + threadIdx.x;
+            if (v >= nv) continue;
+#pragma unroll
+            for (uint32_t w = 0; w < 16; ++w) {
+                const uint64_t pos = a0 + 16ull * v + w;
+                if (pos >= b0 && pos < b1) {
+                    const uint64_t x0 = pos - b0;
+                    s_pat[rev ? len - 1 - x0 : x0] = s.enc[(x[u][w >> 2] >> (8 * (w & 3))) & 0xffu];
+                }
+            }
+        }
     }
     return true;
 }
 
 template <typename P>
 __device__ __forceinline__ PatView pattern_view(const Tables<P> &s, const uint8_t *s_pat, bool staged,
-                                                const uint8_t *bytes, const uint64_t *offs, uint64_t i,
-                                                uint64_t b0, uint64_t b1, bool rev) {
+                                                const uint8_t *bytes, uint64_t beg, uint64_t end, uint64_t b0,
+                                                uint64_t b1, bool rev) {
     PatView pv;
-    const uint64_t beg = offs[i], end = offs[i + 1];
     pv.m = end - beg;
     pv.rev = rev;
     pv.raw = bytes + beg;
@@ -118,12 +146,12 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
     __syncthreads();
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
     const uint64_t first = (uint64_t)blockIdx.x * 256u;
-    uint64_t b0, b1;
-    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, b0, b1);
+    uint64_t beg, end, b0, b1;
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, beg, end, b0, b1);
     __syncthreads();
     const uint64_t i = first + threadIdx.x;
     if (i >= npat) return;
-    const PatView pv = pattern_view(s, s_pat, staged, bytes, offs, i, b0, b1, rev);
+    const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
     P lo, hi, rloc;
     uint64_t mask;
     uint32_t mode;
@@ -173,8 +201,9 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
 
     // ---- 1. SA interval of every pattern of the tile ----------------------
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
-    uint64_t b0, b1;
-    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, b0, b1);
+    uint64_t beg, end, b0, b1;
+    const bool staged =
+        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end, b0, b1);
     __syncthreads();
     FMX_STAMP(1, __builtin_amdgcn_s_memrealtime());
     FMX_STAMP(5, g);
@@ -183,7 +212,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     uint64_t mask = 0;
     uint32_t mode = kHitRows;
     if (i < npat) {
-        const PatView pv = pattern_view(s, s_pat, staged, bytes, offs, i, b0, b1, rev);
+        const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
         const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
         if (bad) atomicOr(a.status, bad);
         if (out_cnt) out_cnt[i] = hi - lo;
@@ -246,9 +275,9 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
 
     // ---- 3. locate walk, rows of the wave's 64 patterns dealt to its lanes --
     const int lane = threadIdx.x & 63;
-    const uint64_t start = __shfl(my_off, 0);
-    const uint64_t end = __shfl(my_off + cnt, 63);
-    for (uint64_t t0 = start; t0 < end; t0 += 64) {
+    const uint64_t w_start = __shfl(my_off, 0);
+    const uint64_t w_end = __shfl(my_off + cnt, 63);
+    for (uint64_t t0 = w_start; t0 < w_end; t0 += 64) {
         const uint64_t t = t0 + lane;
         int jl = 0;  // largest lane whose first slot is <= t
 #pragma unroll
@@ -261,7 +290,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
         const P rloc_j = __shfl(rloc, jl);
         const uint32_t mode_j = (uint32_t)__shfl((int)mode, jl);
         const uint64_t mask_j = __shfl(mask, jl);
-        if (t < end) {
+        if (t < w_end) {
             const uint64_t q = t - off_j;  // occurrence q of pattern jl
             P loc;
             if (mode_j == kHitOne) {
