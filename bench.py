@@ -80,9 +80,10 @@ def phase_stamps(pkg, ix, step, B, out_path):
     live = np.arange(waves) * 64 < B
     t = t[live]
     t0 = t[:, 0].min()
-    rel = (t[:, :5] - t0) / 100.0  # us
+    rel = (t - t0) / 100.0  # us
     pct = lambda x: {q: round(float(np.percentile(x, q)), 2) for q in (0, 10, 50, 90, 100)}
-    res = {"waves": int(live.sum()), "entry": pct(rel[:, 0]), "staged": pct(rel[:, 1]), "searched": pct(rel[:, 2]),
+    res = {"waves": int(live.sum()), "entry": pct(rel[:, 0]), "tile_id": pct(rel[:, 6]), "offs_loaded": pct(rel[:, 7]),
+           "staged": pct(rel[:, 1]), "searched": pct(rel[:, 2]),
            "offsets": pct(rel[:, 3]), "done": pct(rel[:, 4]),
            "stage_us": pct(rel[:, 1] - rel[:, 0]), "search_us": pct(rel[:, 2] - rel[:, 1]),
            "lookback_us": pct(rel[:, 3] - rel[:, 2]), "locate_us": pct(rel[:, 4] - rel[:, 3])}

@@ -30,8 +30,9 @@ namespace fmx {
 
 #ifdef FMX_PHASE_STAMPS
 // Diagnostic build only: s_memrealtime (100 MHz) per wave at each phase of
-// k_locate: [0] entry, [1] patterns staged, [2] search done, [3] offsets
-// known (look-back done), [4] locations written, [5] tile id.
+// k_locate: [0] entry, [6] tile id known, [7] pattern offsets loaded,
+// [1] patterns staged, [2] search done, [3] offsets known (look-back done),
+// [4] locations written, [5] tile id.
 constexpr uint32_t kStampWaves = 1u << 17, kStampSlots = 8;
 __device__ uint64_t g_stamps[kStampWaves * kStampSlots];
 #define FMX_STAMP(slot, v)                                                                   \
@@ -94,6 +95,10 @@ __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pa
     beg = i < npat ? offs[i] : 0;
     end = i < npat ? offs[i + 1] : 0;
     const uint64_t len = b1 - b0;
+#ifdef FMX_PHASE_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    FMX_STAMP(7, __builtin_amdgcn_s_memrealtime() + (beg & 0) + (end & 0) + (len & 0));
+#endif
     if (len > stage_bytes) return false;
     using V4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint64_t a0 = b0 & ~15ull;
@@ -193,6 +198,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
         s_par = par;
     }
     __syncthreads();
+    FMX_STAMP(6, __builtin_amdgcn_s_memrealtime());
     const uint32_t g = s_tile;
     uint64_t *cur = tiles + (uint64_t)s_par * tiles_cap;
     uint64_t *nxt = tiles + (uint64_t)(s_par ^ 1u) * tiles_cap;
