@@ -181,29 +181,21 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     __shared__ uint64_t s_scan[4];
     __shared__ uint64_t s_prefix;
-    __shared__ uint32_t s_tile, s_par;
+    __shared__ uint32_t s_par;
     FMX_STAMP(0, __builtin_amdgcn_s_memrealtime());
     stage_tables(a, s);
     const uint32_t G = (uint32_t)((npat + 255) / 256);
-    if (threadIdx.x == 0) {
-        // Dynamic tile id: tiles are numbered in the order workgroups start, so
-        // a look-back only ever waits on workgroups that are already running.
-        const uint32_t par = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t g = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (g == G - 1) {  // last id handed out: reset for the next launch
-            __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl[1], par ^ 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_tile = g;
-        s_par = par;
-    }
-    __syncthreads();
+    // Tile g = blockIdx.x.  The look-back below waits only on lower tiles, and
+    // workgroups are dispatched in increasing id order (per XCD, round-robin
+    // over XCDs), so every tile waited on is running or done.  (A ticket
+    // taken with one device-scope atomic per workgroup would guarantee the
+    // same at the price of 391 serialised atomics on one address before any
+    // pattern is read — 5-10 us of a 30 us launch, measured.)
+    const uint32_t g = blockIdx.x;
+    // Which of the two tile-status buffers this launch uses: read now, needed
+    // after the search (the last workgroup to finish flips it, see the end).
+    if (threadIdx.x == 0) s_par = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     FMX_STAMP(6, __builtin_amdgcn_s_memrealtime());
-    const uint32_t g = s_tile;
-    uint64_t *cur = tiles + (uint64_t)s_par * tiles_cap;
-    uint64_t *nxt = tiles + (uint64_t)(s_par ^ 1u) * tiles_cap;
-    // clear the other tile buffer for the next launch (this launch never reads it)
-    for (uint64_t x = (uint64_t)g * 256 + threadIdx.x; x < tiles_cap; x += (uint64_t)G * 256) nxt[x] = 0;
 
     // ---- 1. SA interval of every pattern of the tile ----------------------
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
@@ -228,7 +220,11 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
 
     // ---- 2. output offsets: single-pass scan with decoupled look-back -----
     uint64_t agg;
-    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);
+    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);  // (its barriers publish s_par)
+    uint64_t *cur = tiles + (uint64_t)s_par * tiles_cap;
+    uint64_t *nxt = tiles + (uint64_t)(s_par ^ 1u) * tiles_cap;
+    // clear the other tile buffer for the next launch (this launch never reads it)
+    for (uint64_t x = (uint64_t)g * 256 + threadIdx.x; x < tiles_cap; x += (uint64_t)G * 256) nxt[x] = 0;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         if (g == 0) {
@@ -316,6 +312,15 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     __builtin_amdgcn_s_waitcnt(0);
 #endif
     FMX_STAMP(4, __builtin_amdgcn_s_memrealtime());
+    // The last workgroup out flips the buffer parity for the next launch on
+    // this workspace and resets the counter (kernel boundaries publish both).
+    if (threadIdx.x == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == G - 1) {
+            __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[1], s_par ^ 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 // ------------------------------------------------------------ deep k-mer table
