@@ -71,8 +71,9 @@ typedef struct fmx_layout {
 #define FMX_OCC_INTERLEAVED 1u /* checkpoints + bit planes re-laid out into one HBM line per block */
 #define FMX_OPT_DEEP_LUT 2u    /* a K-mer interval table (K > the blob's k), built on the GPU by
                                   breadth-first backward search; replaces the first LF steps.
-                                  K = the largest with sigma^K * 2P bytes <= FMX_DEEP_LUT_MB
-                                  (environment, default 16384) */
+                                  Indexed by the S symbols that occur in the text: K = the
+                                  largest with S^K * 2P bytes <= FMX_DEEP_LUT_MB (environment;
+                                  default 40960, capped at a quarter of free HBM) */
 #define FMX_OPT_FULL_SA 4u     /* the full suffix array (n x P), recovered on the GPU by walking every
                                   row to its sample: a location is one read, no walk            */
 #define FMX_OPT_TEXT 8u        /* the text (n symbol indices), recovered from the full SA; once an
@@ -83,8 +84,13 @@ typedef struct fmx_layout {
                                   sigma+1; an interval of at most FMX_SCAN_ROWS rows (environment,
                                   default 32) is finished by one contiguous scan of its records
                                   instead of LF steps (implies FMX_OPT_FULL_SA | FMX_OPT_TEXT)    */
+#define FMX_OPT_LUT_ROWS 32u   /* deep-table entries whose interval is a single row hold that row's
+                                  SA value and the symbols preceding its suffix instead of the
+                                  interval: such a pattern is settled by that one read (plus a
+                                  text compare beyond the packed symbols).  Needs FMX_OPT_DEEP_LUT
+                                  and FMX_OPT_TEXT, and n < 2^31 for u32 positions            */
 #define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | \
-                         FMX_OPT_ROW_CONTEXT)
+                         FMX_OPT_ROW_CONTEXT | FMX_OPT_LUT_ROWS)
 
 typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
 

@@ -315,10 +315,12 @@ def _layout(position: Position, block: _Block, encoder) -> _n.fmx_layout:
     return _n.fmx_layout(position.nbytes, block.planes, block.vector.bits, encoder.ENCODER)
 
 
-def _options(occ: str, deep_lut: bool, full_sa: bool = True, text: bool = True, context: bool = True) -> int:
+def _options(occ: str, deep_lut: bool, full_sa: bool = True, text: bool = True, context: bool = True,
+             lut_rows: bool = True) -> int:
     mode = _n.FMX_OCC_INTERLEAVED if occ == "interleaved" else _n.FMX_OCC_BLOB
     return (mode | (_n.FMX_OPT_DEEP_LUT if deep_lut else 0) | (_n.FMX_OPT_FULL_SA if full_sa else 0)
-            | (_n.FMX_OPT_TEXT if text else 0) | (_n.FMX_OPT_ROW_CONTEXT if context else 0))
+            | (_n.FMX_OPT_TEXT if text else 0) | (_n.FMX_OPT_ROW_CONTEXT if context else 0)
+            | (_n.FMX_OPT_LUT_ROWS if lut_rows else 0))
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -343,7 +345,7 @@ class FmIndex:
     def load(cls, blob, position: Position = u32, block: Optional[_Block] = None,
              text_encoder=text_encoders.EncodingTable, device: int = 0,
              occ: str = "interleaved", deep_lut: bool = True, full_sa: bool = True, text: bool = True,
-             context: bool = True, options: Optional[int] = None) -> "FmIndex":
+             context: bool = True, lut_rows: bool = True, options: Optional[int] = None) -> "FmIndex":
         """``FmIndex::load`` (load_from_blob.rs:28-85): validate, then copy the
         blob to HBM once and derive the device structures chosen by the flags
         (results are identical with any of them):
@@ -353,7 +355,8 @@ class FmIndex:
         full suffix array (FMX_OPT_FULL_SA); `text` — the recovered text for
         single-row tail verification (FMX_OPT_TEXT); `context` — row records
         {SA, preceding symbols} so that small intervals finish with one scan
-        (FMX_OPT_ROW_CONTEXT).  `options` overrides all."""
+        (FMX_OPT_ROW_CONTEXT); `lut_rows` — single-row deep-table entries
+        that hold the row's location (FMX_OPT_LUT_ROWS).  `options` overrides all."""
         block = block or blocks.Block2(Vector.U64)
         if isinstance(text_encoder, type):
             text_encoder = text_encoder.__new__(text_encoder)
@@ -364,7 +367,7 @@ class FmIndex:
             arr = a2
         h = C.c_void_p()
         exp, act = C.c_uint64(), C.c_uint64()
-        mode = options if options is not None else _options(occ, deep_lut, full_sa, text, context)
+        mode = options if options is not None else _options(occ, deep_lut, full_sa, text, context, lut_rows)
         st = _n.lib().fmx_load(_ptr(arr), arr.size, _layout(position, block, text_encoder), device, mode,
                                C.byref(h), C.byref(exp), C.byref(act))
         if st == _n.FMX_E_FORMAT:
@@ -380,14 +383,15 @@ class FmIndex:
     def load_device(cls, d_blob: int, blob_len: int, position: Position = u32,
                     block: Optional[_Block] = None, text_encoder=text_encoders.EncodingTable,
                     device: int = 0, occ: str = "interleaved", deep_lut: bool = True, full_sa: bool = True,
-                    text: bool = True, context: bool = True, options: Optional[int] = None) -> "FmIndex":
+                    text: bool = True, context: bool = True, lut_rows: bool = True,
+                    options: Optional[int] = None) -> "FmIndex":
         """Load a blob already resident in HBM (borrowed, must outlive the index)."""
         block = block or blocks.Block2(Vector.U64)
         if isinstance(text_encoder, type):
             text_encoder = text_encoder.__new__(text_encoder)
         h = C.c_void_p()
         exp, act = C.c_uint64(), C.c_uint64()
-        mode = options if options is not None else _options(occ, deep_lut, full_sa, text, context)
+        mode = options if options is not None else _options(occ, deep_lut, full_sa, text, context, lut_rows)
         st = _n.lib().fmx_load_device(C.c_void_p(d_blob), blob_len, _layout(position, block, text_encoder),
                                       device, mode, C.byref(h), C.byref(exp), C.byref(act))
         if st == _n.FMX_E_FORMAT:

@@ -254,16 +254,28 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         }
     }
     ix->options = ix->occ_mode;
-    if (options & FMX_OPT_DEEP_LUT) {
-        // the largest K with sigma^K * 2P <= budget, deeper than the blob's k
-        uint64_t budget = 16384ull << 20;
+    // deep-table digits: the symbols that occur in the text (a pattern holding
+    // any other symbol is left to the blob's seed and the LF loop)
+    uint32_t S = 0;
+    for (uint32_t c = 0; c < (uint32_t)kMaxSigma; ++c) q.dlut_dig[c] = kNoDigit;
+    for (uint32_t c = 0; c < v.sigma; ++c)
+        if (v.C[c + 1] > v.C[c]) {
+            q.dlut_dig[c] = (uint8_t)S;
+            q.dlut_sym[S++] = (uint8_t)c;
+        }
+    if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
+        // the largest K with S^K * 2P <= budget, deeper than the blob's k;
+        // budget: FMX_DEEP_LUT_MB, else 40 GiB capped at a quarter of free HBM
+        uint64_t budget = 40960ull << 20;
+        size_t hfree = 0, htotal = 0;
+        if (hipMemGetInfo(&hfree, &htotal) == hipSuccess) budget = std::min<uint64_t>(budget, hfree / 4);
         if (const char *env = getenv("FMX_DEEP_LUT_MB")) budget = strtoull(env, nullptr, 10) << 20;
         const uint64_t per = 2ull * v.L.pos_bytes;
         uint32_t K = 0;
         uint64_t cnt = 1;
-        while (K < 32 && cnt <= budget / per / v.sigma) { cnt *= v.sigma; ++K; }
-        if (v.sigma < 2) K = 0;
-        if (K > v.k && v.n > 0) {
+        while (K < 32 && cnt <= budget / per / S) { cnt *= S; ++K; }
+        if (K > v.k) {
+            q.dlut_sigma = S;
             if (build_deep_lut(ix, K, ix->stream) != hipSuccess) return FMX_E_DEVICE;
             q.dlut = ix->d_dlut;
             q.dlut_k = K;
@@ -299,6 +311,17 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
             if (build_row_context(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
             ix->options |= FMX_OPT_ROW_CONTEXT;
         }
+    }
+    // single-row deep-table entries: the row flag needs n < 2^(8P-1)
+    if ((options & FMX_OPT_LUT_ROWS) && q.dlut && q.text && q.safull &&
+        (v.L.pos_bytes == 8 || v.n < (1ull << 31))) {
+        uint32_t bps = 1;
+        while ((1u << bps) < v.sigma + 2) ++bps;  // digits 0..sigma stored, sigma+1 = "no match"
+        q.dlut_bps = bps;
+        q.dlut_ctx = (8 * v.L.pos_bytes - 1) / bps;
+        if (build_dlut_rows(ix, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+        q.dlut_rows = 1;
+        ix->options |= FMX_OPT_LUT_ROWS;
     }
     return FMX_OK;
 }

@@ -184,6 +184,7 @@ struct Occ {
 template <typename P>
 struct Tables {
     uint8_t enc[256];
+    uint8_t dig[kMaxSigma];  // symbol -> deep-table digit (QueryArgs::dlut_dig)
     P C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
 };
@@ -262,11 +263,11 @@ FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo
     const uint64_t span = a.wpow[Cl - L];
     const uint64_t clo = code * span, chi = clo + span;  // ctx in [clo, chi)
     // Records are read as 16-B vectors, NV of them issued before any is used
-    // (one round covers 8 u32 / 4 u64 rows; the row-record buffer is padded so
+    // (one round covers 16 u32 / 8 u64 rows; the row-record buffer is padded so
     // the last vector never leaves it).  Bits of msk are rows relative to lo.
     using V4 = uint32_t __attribute__((ext_vector_type(4)));
     constexpr uint32_t RPV = 16 / (2 * sizeof(P));
-    constexpr uint32_t NV = 4;
+    constexpr uint32_t NV = 8;
     const V4 *vec = reinterpret_cast<const V4 *>(a.safull);
     const uint64_t v0 = (uint64_t)lo / RPV, v1 = ((uint64_t)hi + RPV - 1) / RPV;
     uint64_t msk = 0;
@@ -322,6 +323,46 @@ FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo
     }
 }
 
+// Marks a single-row entry of the deep k-mer table (FMX_OPT_LUT_ROWS): the top
+// bit of the first word, which no row number has (n < 2^(8P-1) is required).
+template <typename P>
+FMX_HD constexpr P row_flag() { return P(1) << (8 * sizeof(P) - 1); }
+
+// Single-row deep-table entry {row_flag | ctx, x}: the last K symbols of the
+// pattern occur once in the text, as the suffix at x = SA of that row, and ctx
+// packs T[x-1], T[x-2], ..., T[x-dlut_ctx] (symbol + 1, 0 before the text
+// start), dlut_bps bits each, the nearest in the low bits.  The LF loop over
+// P[0..idx) (with_slice.rs:27-31) keeps that one row while every symbol equals
+// the text symbol before the suffix and empties at the first (highest)
+// position that does not — where it reads, and for PassThrough rejects, that
+// pattern symbol.  Here the nearest dlut_ctx positions are compared in one
+// XOR and the rest against the text.
+template <typename P>
+FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w0, P w1, P &lo, P &hi, P &rloc,
+                        uint32_t &mode) {
+    const uint32_t bps = a.dlut_bps, Ld = a.dlut_ctx;
+    const uint64_t x = (uint64_t)w1;
+    const uint64_t L = idx < Ld ? idx : Ld;
+    uint64_t pc = 0;
+    for (uint64_t j = 0; j < L; ++j) {
+        const uint32_t c = pv.at(idx - 1 - j);
+        const uint64_t d = c < a.sigma ? c + 1 : a.sigma + 1;  // sigma + 1: never a stored digit
+        pc |= d << (bps * j);
+    }
+    const uint64_t keep = L * bps >= 64 ? ~0ull : (1ull << (L * bps)) - 1;
+    const uint64_t diff = (pc ^ (uint64_t)(w0 & (P)~row_flag<P>())) & keep;
+    int64_t jm;
+    if (diff) jm = (int64_t)(idx - 1 - (uint64_t)__builtin_ctzll(diff) / bps);
+    else jm = idx > Ld ? tail_mismatch<P>(a, pv, idx, x, idx - Ld) : -1;
+    mode = kHitOne;
+    lo = 0;
+    hi = 0;
+    if (jm >= 0) return pv.at((uint64_t)jm) >= a.sigma ? kStatusSymbol : 0;
+    hi = 1;
+    rloc = (P)(x - idx);
+    return 0;
+}
+
 // k-mer seed + LF loop: FmIndex::get_pos_range (with_slice.rs:21-33).
 // Returns status bits (0 = ok).  The result is the interval [lo, hi) with
 // mode kHitRows, or (derived structures) an interval finished early: a
@@ -339,25 +380,36 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
     mask = 0;
     mode = kHitRows;
     if (m == 0) return kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
-    uint64_t idx;
+    uint64_t idx = 0;
     uint32_t bad = 0;
+    bool seeded = false;
     if (a.dlut != nullptr && m >= a.dlut_k) {
-        // deep k-mer table: the SA interval of the last K symbols in one read
-        // (the same interval K-k more LF steps from the blob's seed reach)
-        const uint32_t K = a.dlut_k;
+        // deep k-mer table over the symbols that occur in the text: the SA
+        // interval of the last K symbols in one read (the interval K-k more LF
+        // steps from the blob's seed reach).  A symbol that does not occur (or
+        // is >= sigma) leaves the pattern to the blob's seed and the LF loop,
+        // which empty the interval — or reject the symbol — exactly there.
+        const uint32_t K = a.dlut_k, S = a.dlut_sigma;
         uint64_t code = 0;
+        uint32_t miss = 0;
 #pragma unroll 4
         for (uint32_t j = 0; j < K; ++j) {
             const uint32_t c = pv.at(m - K + j);
-            bad |= c >= sigma;
-            code = code * sigma + c;
+            const uint32_t d = c < sigma ? s.dig[c] : kNoDigit;
+            miss |= d == kNoDigit;
+            code = code * S + d;
         }
-        if (bad) return kStatusSymbol;
-        const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
-        lo = dl[0];
-        hi = dl[1];
-        idx = m - K;
-    } else {
+        if (!miss) {
+            const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
+            const P w0 = dl[0], w1 = dl[1];
+            idx = m - K;
+            if (a.dlut_rows && (w0 & row_flag<P>())) return one_row<P>(a, pv, idx, w0, w1, lo, hi, rloc, mode);
+            lo = w0;
+            hi = w1;
+            seeded = true;
+        }
+    }
+    if (!seeded) {
         // seed: count_array.rs:203-233
         uint64_t code = 0, e;
         const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;

@@ -62,8 +62,12 @@ struct QueryArgs {
     uint64_t sr_magic;                   // ceil(2^64 / sr) for sr not a power of two
     uint32_t strict;          // PassThrough: bytes >= sigma are an error
     uint32_t rec_bytes;       // interleaved record size
-    const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every sigma^dlut_k string, or null
+    const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every dlut_sigma^dlut_k string, or null
     uint32_t dlut_k;
+    uint32_t dlut_sigma;      // digits of the table: the symbols that occur in the text (C[c] < C[c+1])
+    uint32_t dlut_rows;       // single-row entries are {row_flag | preceding symbols, SA} (FMX_OPT_LUT_ROWS)
+    uint32_t dlut_bps;        // bits per packed preceding symbol in a single-row entry
+    uint32_t dlut_ctx;        // packed preceding symbols per single-row entry
     uint32_t pad_;
     const uint8_t *safull;    // full suffix array: SA[r] = P at safull[r * sa_stride] (FMX_OPT_FULL_SA), or null
     const uint8_t *text;      // text as symbol indices [u8; n] (FMX_OPT_TEXT), or null
@@ -75,7 +79,11 @@ struct QueryArgs {
     uint64_t C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
     uint8_t enc[256];
+    uint8_t dlut_dig[kMaxSigma];  // symbol -> digit of the deep table (kNoDigit: absent from the text)
+    uint8_t dlut_sym[kMaxSigma];  // digit -> symbol
 };
+
+constexpr uint8_t kNoDigit = 0xFF;
 
 // Device status bits
 constexpr uint32_t kStatusEmpty = 1u;
@@ -141,6 +149,9 @@ uint64_t locate_tiles_cap(uint64_t n);
 hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
 // Build the deep k-mer table (FMX_OPT_DEEP_LUT) for K into ix->d_dlut.
 hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream);
+// Turn its single-row intervals into {row_flag | preceding symbols, SA} entries
+// (FMX_OPT_LUT_ROWS; needs the full SA and the text).
+hipError_t build_dlut_rows(fmx_index *ix, hipStream_t stream);
 // Recover the full suffix array into ix->d_safull (FMX_OPT_FULL_SA).
 hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream);
 // Recover the text (symbol indices) into ix->d_text from d_safull (FMX_OPT_TEXT).

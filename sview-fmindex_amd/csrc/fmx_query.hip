@@ -48,6 +48,7 @@ template <typename P>
 __device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s) {
     const int t = threadIdx.x;
     s.enc[t] = a.enc[t];
+    if (t < kMaxSigma) s.dig[t] = a.dlut_dig[t];
     if ((uint32_t)t <= a.sigma) s.C[t] = (P)a.C[t];
     if ((uint32_t)t < a.k) s.mult[t] = a.mult[t];
 }
@@ -99,6 +100,8 @@ __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pa
     __builtin_amdgcn_s_waitcnt(0);
     FMX_STAMP(7, __builtin_amdgcn_s_memrealtime() + (beg & 0) + (end & 0) + (len & 0));
 #endif
+    // the encoding table (stage_tables, written by every thread) is read below
+    __syncthreads();
     if (len > stage_bytes) return false;
     using V4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint64_t a0 = b0 & ~15ull;
@@ -325,20 +328,22 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
 
 // ------------------------------------------------------------ deep k-mer table
 
+// The table's digits are the S symbols that occur in the text (dlut_sym).
 // Level 1: the interval of each single symbol c is [C[c], C[c+1]) (the root,
 // the empty string, is full row 0..n which the reduced row numbering cannot
 // represent, so level 1 is written directly; count_array.rs:139-145).
 template <typename P>
 __global__ void k_dlut_root(const QueryArgs a, P *__restrict__ out) {
-    const uint32_t c = threadIdx.x;
-    if (c < a.sigma) {
-        out[2 * c] = (P)a.C[c];
-        out[2 * c + 1] = (P)a.C[c + 1];
+    const uint32_t d = threadIdx.x;
+    if (d < a.dlut_sigma) {
+        const uint32_t c = a.dlut_sym[d];
+        out[2 * d] = (P)a.C[c];
+        out[2 * d + 1] = (P)a.C[c + 1];
     }
 }
 
-// Level j -> j+1: child string cS has code c*sigma^j + code(S); its interval
-// is one LF step (next_pos_range, locate/mod.rs:39-45) from S's.
+// Level j -> j+1: child string cS has code digit(c)*S^j + code(S); its
+// interval is one LF step (next_pos_range, locate/mod.rs:39-45) from S's.
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *__restrict__ parent, uint64_t np,
                                                     P *__restrict__ child) {
@@ -347,16 +352,35 @@ __global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *
     if (x >= np) return;
     const P lo = parent[2 * x], hi = parent[2 * x + 1];
     const P sent = (P)a.sentinel;
-    for (uint32_t c = 0; c < a.sigma; ++c) {
+    for (uint32_t d = 0; d < a.dlut_sigma; ++d) {
+        const uint32_t c = a.dlut_sym[d];
         P clo = 0, chi = 0;
         if (lo < hi) {
             const P pre = (P)a.C[c];
             clo = pre + O::rank_at(a, lo + (lo < sent ? P(1) : P(0)), c);
             chi = pre + O::rank_at(a, hi + (hi < sent ? P(1) : P(0)), c);
         }
-        P *dst = child + 2 * ((uint64_t)c * np + x);
+        P *dst = child + 2 * ((uint64_t)d * np + x);
         dst[0] = clo;
         dst[1] = chi;
+    }
+}
+
+// Single-row entries (FMX_OPT_LUT_ROWS): an interval of exactly one row r
+// becomes {row_flag | T[x-1], T[x-2], ..., T[x-dlut_ctx] packed, x = SA[r]}
+// (see one_row in fmx_device.hpp).
+template <typename P>
+__global__ __launch_bounds__(256) void k_dlut_rows(const QueryArgs a, uint64_t entries, P *__restrict__ dl) {
+    const P *sa = reinterpret_cast<const P *>(a.safull);
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < entries; e += (uint64_t)gridDim.x * 256) {
+        const P lo = dl[2 * e], hi = dl[2 * e + 1];
+        if (!(lo < hi && hi - lo == P(1))) continue;
+        const uint64_t x = (uint64_t)sa[(uint64_t)lo * a.sa_stride];
+        uint64_t v = 0;
+        for (uint32_t j = 1; j <= a.dlut_ctx; ++j)
+            v |= (j <= x ? (uint64_t)a.text[x - j] + 1 : 0ull) << (a.dlut_bps * (j - 1));
+        dl[2 * e] = row_flag<P>() | (P)v;
+        dl[2 * e + 1] = (P)x;
     }
 }
 
@@ -516,7 +540,7 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
 }
 
 hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream) {
-    const uint64_t sigma = ix->bv.sigma, pb = ix->bv.L.pos_bytes;
+    const uint64_t sigma = ix->qa.dlut_sigma, pb = ix->bv.L.pos_bytes;
     uint64_t total = 1;
     for (uint32_t j = 0; j < K; ++j) total *= sigma;
     uint8_t *tmp = nullptr;
@@ -550,6 +574,19 @@ hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream) {
 static inline unsigned grid_stride_for(uint64_t n) {
     const uint64_t g = (n + 255) / 256;
     return (unsigned)(g < 65536 ? (g ? g : 1) : 65536);
+}
+
+hipError_t build_dlut_rows(fmx_index *ix, hipStream_t stream) {
+    const uint64_t entries = ix->dlut_bytes / (2ull * ix->bv.L.pos_bytes);
+    if (ix->bv.L.pos_bytes == 4)
+        hipLaunchKernelGGL((k_dlut_rows<uint32_t>), dim3(grid_stride_for(entries)), dim3(256), 0, stream, ix->qa,
+                           entries, (uint32_t *)ix->d_dlut);
+    else
+        hipLaunchKernelGGL((k_dlut_rows<uint64_t>), dim3(grid_stride_for(entries)), dim3(256), 0, stream, ix->qa,
+                           entries, (uint64_t *)ix->d_dlut);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e;
 }
 
 hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream) {

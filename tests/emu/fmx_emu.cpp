@@ -59,34 +59,47 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
         a.occ = occ.data();
     }
     using O = Occ<P, N, VB, REC>;
-    // deep k-mer table (k_dlut_root / k_dlut_level)
+    // deep k-mer table over the symbols that occur in the text (k_dlut_root / k_dlut_level)
+    uint32_t S = 0;
+    for (uint32_t c = 0; c < (uint32_t)kMaxSigma; ++c) a.dlut_dig[c] = kNoDigit;
+    for (uint32_t c = 0; c < ox.sigma; ++c)
+        if (a.C[c + 1] > a.C[c]) {
+            a.dlut_dig[c] = (uint8_t)S;
+            a.dlut_sym[S++] = (uint8_t)c;
+        }
+    memcpy(t.dig, a.dlut_dig, sizeof(t.dig));
     std::vector<P> lut, lev;
-    if (options & 2u) {
+    if ((options & 2u) && S >= 2 && ox.n > 0) {
         uint64_t budget = 1ull << 20;  // what tests/test_gpu.py sets (FMX_DEEP_LUT_MB=1)
         uint32_t K = 0;
         uint64_t cnt = 1;
-        while (K < 32 && cnt <= budget / (2 * sizeof(P)) / ox.sigma) { cnt *= ox.sigma; ++K; }
-        if (ox.sigma >= 2 && K > ox.k && ox.n > 0) {
-            lev.assign(2 * ox.sigma, 0);
-            for (uint32_t c = 0; c < ox.sigma; ++c) { lev[2 * c] = (P)a.C[c]; lev[2 * c + 1] = (P)a.C[c + 1]; }
-            uint64_t np = ox.sigma;
+        while (K < 32 && cnt <= budget / (2 * sizeof(P)) / S) { cnt *= S; ++K; }
+        if (K > ox.k) {
+            lev.assign(2 * S, 0);
+            for (uint32_t d = 0; d < S; ++d) {
+                lev[2 * d] = (P)a.C[a.dlut_sym[d]];
+                lev[2 * d + 1] = (P)a.C[a.dlut_sym[d] + 1];
+            }
+            uint64_t np = S;
             for (uint32_t j = 1; j < K; ++j) {
-                std::vector<P> nxt(2 * np * ox.sigma, 0);
+                std::vector<P> nxt(2 * np * S, 0);
                 for (uint64_t x = 0; x < np; ++x) {
                     const P lo = lev[2 * x], hi = lev[2 * x + 1];
                     if (!(lo < hi)) continue;
-                    for (uint32_t c = 0; c < ox.sigma; ++c) {
+                    for (uint32_t d = 0; d < S; ++d) {
+                        const uint32_t c = a.dlut_sym[d];
                         const P pre = (P)a.C[c];
-                        nxt[2 * (c * np + x)] = pre + O::rank_at(a, lo + (lo < (P)a.sentinel ? P(1) : P(0)), c);
-                        nxt[2 * (c * np + x) + 1] = pre + O::rank_at(a, hi + (hi < (P)a.sentinel ? P(1) : P(0)), c);
+                        nxt[2 * (d * np + x)] = pre + O::rank_at(a, lo + (lo < (P)a.sentinel ? P(1) : P(0)), c);
+                        nxt[2 * (d * np + x) + 1] = pre + O::rank_at(a, hi + (hi < (P)a.sentinel ? P(1) : P(0)), c);
                     }
                 }
                 lev.swap(nxt);
-                np *= ox.sigma;
+                np *= S;
             }
             lut.swap(lev);
             a.dlut = reinterpret_cast<const uint8_t *>(lut.data());
             a.dlut_k = K;
+            a.dlut_sigma = S;
         }
     }
     // full SA (k_full_sa), text (k_text), row contexts (k_row_ctx)
@@ -128,6 +141,23 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
                 safull[2 * r + 1] = (P)v;
             }
         }
+    }
+    // single-row deep-table entries (k_dlut_rows)
+    if ((options & 32u) && a.dlut && a.text && safull && (sizeof(P) == 8 || ox.n < (1ull << 31))) {
+        uint32_t bps = 1;
+        while ((1u << bps) < ox.sigma + 2) ++bps;
+        a.dlut_bps = bps;
+        a.dlut_ctx = (8 * sizeof(P) - 1) / bps;
+        for (uint64_t e = 0; e < lut.size() / 2; ++e) {
+            const P lo = lut[2 * e], hi = lut[2 * e + 1];
+            if (!(lo < hi && hi - lo == P(1))) continue;
+            const uint64_t x = (uint64_t)safull[(uint64_t)lo * a.sa_stride];
+            uint64_t v = 0;
+            for (uint32_t j = 1; j <= a.dlut_ctx; ++j) v |= (j <= x ? (uint64_t)text[x - j] + 1 : 0ull) << (bps * (j - 1));
+            lut[2 * e] = row_flag<P>() | (P)v;
+            lut[2 * e + 1] = (P)x;
+        }
+        a.dlut_rows = 1;
     }
     // queries (k_locate without the scan: outputs are in pattern order anyway)
     uint64_t out = 0;
@@ -209,7 +239,7 @@ int by_n(const orc_index &ox, uint32_t rec, uint32_t options, const uint8_t *b, 
 extern "C" {
 
 // options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text,
-// 16 row contexts); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
+// 16 row contexts, 32 single-row deep-table entries); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
 // Outputs are u64: counts[npat] and the concatenated locations.
 int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
                uint32_t encoder, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,

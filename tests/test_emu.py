@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 EMU = os.path.join(HERE, "emu", "libfmx_emu.so")
 # fmx_load option bits; bits 8.. set the row-scan limit (FMX_SCAN_ROWS)
 OPTIONS = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 2 | 8, 31, 16, 1 | 16 | (1 << 8), 2 | 16 | (64 << 8),
-           1 | 2 | 16 | (5 << 8))
+           1 | 2 | 16 | (5 << 8), 2 | 8 | 32, 63, 1 | 2 | 16 | 32 | (3 << 8))
 
 
 @pytest.fixture(scope="module")
@@ -110,4 +110,45 @@ def test_device_code_text_start_and_symbols(emu, O):
                     want = ("err", e.code)
                 st, cnt, locs = emu_locate(emu, blob, layout, options, [p])
                 got = ("ok", sorted(int(x) for x in locs), [int(x) for x in locs]) if st == 0 else ("err", st)
+                assert got == want, (p, options, got, want)
+
+
+def test_device_code_absent_symbols(emu, O):
+    """Symbols of the alphabet that never occur in the text (the deep table is
+    indexed by the occurring ones): patterns holding them anywhere — inside the
+    deep-table window, left of it, in the blob's k-mer window — and, for
+    PassThrough, bytes >= sigma next to them.  Same status and locations as the
+    oracle."""
+    rng = np.random.default_rng(123)
+    # EncodingTable ACGTN, the text has no N (the C2 situation)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4000))
+    for layout in [(4, 3, 64, 0), (8, 3, 128, 0), (4, 3, 32, 0)]:
+        blob = O.build(text, 5, O.layout(*layout[:3]), 3, 2, table)
+        pats = [text[s:s + int(rng.integers(1, 30))] for s in rng.integers(0, 3950, size=300)]
+        for p in list(pats[:120]):
+            j = int(rng.integers(0, len(p)))
+            pats.append(p[:j] + b"N" + p[j + 1:])
+        pats += [b"N", b"NN", b"N" * 20, b"ACGTN" * 4]
+        for options in OPTIONS:
+            check(emu, O, blob, layout, pats, options)
+    # PassThrough sigma 5 over a text of 0..3: symbol 4 is absent, 9 is >= sigma
+    text = bytes(rng.integers(0, 4, size=4000).astype(np.uint8))
+    for layout in [(4, 3, 64, 1), (8, 3, 64, 1)]:
+        blob = O.build(text, 5, O.layout(*layout[:3]), 2, 2, None)
+        orc = O.OracleIndex(blob, O.layout(*layout))
+        pats = [text[s:s + 24] for s in rng.integers(0, 3950, size=60)]
+        muts = []
+        for p in pats:
+            a, b = sorted(int(x) for x in rng.integers(0, len(p), size=2))
+            muts.append(p[:a] + bytes([4]) + p[a + 1:b] + bytes([9]) + p[b + 1:] if a < b else p)
+            muts.append(p[:a] + bytes([9]) + p[a + 1:b] + bytes([4]) + p[b + 1:] if a < b else p)
+        for p in pats + muts:
+            for options in OPTIONS:
+                try:
+                    want = ("ok", orc.locate(p))
+                except O.OracleError as e:
+                    want = ("err", e.code)
+                st, cnt, locs = emu_locate(emu, blob, layout, options, [p])
+                got = ("ok", [int(x) for x in locs]) if st == 0 else ("err", st)
                 assert got == want, (p, options, got, want)

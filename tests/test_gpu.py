@@ -14,10 +14,10 @@ from _util import (ALL_LAYOUTS, encode, occurrences, rand_chr_list, rand_pattern
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 # load options (FMX_OCC_INTERLEAVED=1 | FMX_OPT_DEEP_LUT=2 | FMX_OPT_FULL_SA=4 |
-# FMX_OPT_TEXT=8 | FMX_OPT_ROW_CONTEXT=16): the faithful blob path, each derived
-# structure, everything; a 1 MB table budget makes K > k even on the small test
-# texts (K = 8 for sigma = 4)
-OCC_MODES = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 16, 31)
+# FMX_OPT_TEXT=8 | FMX_OPT_ROW_CONTEXT=16 | FMX_OPT_LUT_ROWS=32): the faithful
+# blob path, each derived structure, everything; a 1 MB table budget makes
+# K > k even on the small test texts (K = 8 for sigma = 4)
+OCC_MODES = (0, 1, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 16, 31, 2 | 8 | 32, 63)
 os.environ.setdefault("FMX_DEEP_LUT_MB", "1")
 
 
@@ -316,7 +316,7 @@ def test_row_context_scan_limits(pkg, O, scan, monkeypatch):
                 + rand_text(rng, chars, 1000, 2000))
         blob = gpu_build(pkg, text, sigma, pb, planes, vb, 3, 3, table)
         pats = [rand_pattern(rng, text, 1, 40) for _ in range(1500)] + [chars[:2] * 5, chars[:2] * 40]
-        for occ in (16, 31):
+        for occ in (16, 31, 63):
             check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
         ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=31)
         info = ix.info()
@@ -329,7 +329,7 @@ def test_row_context_scan_limits(pkg, O, scan, monkeypatch):
     pats += [bytes([9]) + p[1:] for p in pats[:50]] + [p[:10] + bytes([7]) + p[11:] for p in pats[50:100]]
     orc = O.OracleIndex(blob, O.layout(4, 2, 64, 1))
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block2(pkg.Vector.U64), pkg.text_encoders.PassThrough,
-                          options=31)
+                          options=63)
     for p in pats:
         try:
             want = ("ok", orc.locate(p))
@@ -341,3 +341,46 @@ def test_row_context_scan_limits(pkg, O, scan, monkeypatch):
             got = ("err", e.code)
         assert got == want, (p, got, want)
     ix.close()
+
+
+def test_absent_symbols_gpu(pkg, O):
+    """Alphabet symbols that never occur in the text (the deep table is indexed
+    by the occurring ones; C2's N): patterns holding them anywhere, and for
+    PassThrough, bytes >= sigma next to them — same status and locations as
+    the oracle under every load option."""
+    rng = np.random.default_rng(321)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000))
+    for pb, planes, vb in [(4, 3, 64), (8, 3, 128)]:
+        blob = gpu_build(pkg, text, 5, pb, planes, vb, 3, 2, table)
+        pats = [text[s:s + int(rng.integers(1, 30))] for s in rng.integers(0, 19950, size=600)]
+        for p in list(pats[:200]):
+            j = int(rng.integers(0, len(p)))
+            pats.append(p[:j] + b"N" + p[j + 1:])
+        pats += [b"N", b"NN", b"N" * 20, b"ACGTN" * 4]
+        for occ in OCC_MODES:
+            check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+    text = bytes(rng.integers(0, 4, size=20000).astype(np.uint8))
+    blob = gpu_build(pkg, text, 5, 4, 3, 64, 2, 2, None)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 1))
+    pats = [text[s:s + 24] for s in rng.integers(0, 19950, size=40)]
+    muts = []
+    for p in pats:
+        a, b = sorted(int(x) for x in rng.integers(0, len(p), size=2))
+        if a < b:
+            muts.append(p[:a] + bytes([4]) + p[a + 1:b] + bytes([9]) + p[b + 1:])
+            muts.append(p[:a] + bytes([9]) + p[a + 1:b] + bytes([4]) + p[b + 1:])
+    for occ in OCC_MODES:
+        ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), pkg.text_encoders.PassThrough,
+                              options=occ)
+        for p in pats + muts:
+            try:
+                want = ("ok", orc.locate(p))
+            except O.OracleError as e:
+                want = ("err", e.code)
+            try:
+                got = ("ok", [int(x) for x in ix.locate(p)])
+            except pkg.FmxError as e:
+                got = ("err", e.code)
+            assert got == want, (p, occ, got, want)
+        ix.close()
