@@ -69,9 +69,11 @@ def phase_stamps(pkg, ix, step, B, out_path):
     """Diagnostic (FMX_LIB=.../libfmx_stamps.so): per-wave phase timestamps of
     one k_locate launch, summarised as percentiles (10 ns ticks -> us)."""
     import ctypes
+    import torch
     L = pkg._native.lib()
+    torch.cuda.synchronize()
     step()
-    ix.sync()
+    torch.cuda.synchronize()
     waves = (B + 255) // 256 * 4
     buf = np.zeros(waves * 8, np.uint64)
     L.fmx_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
@@ -108,10 +110,19 @@ def parse():
                     help="fmx_load options bit field (FMX_OCC_INTERLEAVED=1|DEEP_LUT=2|FULL_SA=4|TEXT=8|"
                          "ROW_CONTEXT=16); "
                          "default: everything (minus --no-deep-lut)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no HIP events around the launches in the timed region (no roofline)")
+    ap.add_argument("--count-only", action="store_true", help="diagnostic: time fmx_count_batch_async (k_count)")
+    ap.add_argument("--event-every", type=int, default=10,
+                    help="bracket every k-th launch of the timed region with HIP events (an event pair costs the "
+                         "stream several us; 1 = every launch)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batches in flight: step i runs batch i %% S on HIP stream i %% S (each stream its own "
+                         "patterns, outputs and look-back workspace), as a serving loop pipelines batches")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_fetch_size.json"))
     return ap.parse_args()
 
@@ -188,33 +199,55 @@ def main():
     log(f"[rank {rank}] index loaded in {load_s:.2f}s: options={info['options']} deep_lut_k={info['deep_lut_k']} "
         f"device_bytes={info['device_bytes']:,}")
 
-    # ---- patterns: substrings at uniform starts (per-rank seed) ------------
-    pg = torch.Generator(device=dev)
-    pg.manual_seed(args.seed * 1000 + 7 + rank)
-    starts = torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg)
-    d_pat = d_text[(starts[:, None] + torch.arange(m, device=dev)[None, :]).reshape(-1)].contiguous()
-    d_off = (torch.arange(B + 1, device=dev, dtype=torch.int64) * m).contiguous()
+    # ---- patterns: substrings at uniform starts (per-rank, per-stream seed) --
+    # One batch per stream; batch 0 is the one checked against the CPU oracle.
+    S = max(1, args.streams)
     cap = 4 * B + 4096
-    d_loff = torch.zeros(B + 1, dtype=torch.int64, device=dev)
-    d_locs = torch.zeros(cap, dtype=pdt_t, device=dev)
-    d_need = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = ix.locate_workspace_size(B)
-    d_ws = torch.zeros(ws, dtype=torch.uint8, device=dev)
+    batches = []
+    for si in range(S):
+        pg = torch.Generator(device=dev)
+        pg.manual_seed(args.seed * 1000 + 7 + rank + 100003 * si)
+        starts = torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg)
+        batches.append(dict(
+            stream=torch.cuda.Stream(device=dev),
+            starts=starts,
+            pat=d_text[(starts[:, None] + torch.arange(m, device=dev)[None, :]).reshape(-1)].contiguous(),
+            off=(torch.arange(B + 1, device=dev, dtype=torch.int64) * m).contiguous(),
+            loff=torch.zeros(B + 1, dtype=torch.int64, device=dev),
+            locs=torch.zeros(cap, dtype=pdt_t, device=dev),
+            need=torch.zeros(1, dtype=torch.int64, device=dev),
+            ws=torch.zeros(ws, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    b0 = batches[0]
+    starts, d_pat, d_loff, d_locs, d_need = b0["starts"], b0["pat"], b0["loff"], b0["locs"], b0["need"]
+    state = {"i": 0}
+
+    d_cnt = torch.zeros(B, dtype=pdt_t, device=dev)
 
     def step():
-        ix.locate_batch_async(d_pat.data_ptr(), d_off.data_ptr(), B, d_loff.data_ptr(), d_locs.data_ptr(), cap,
-                              d_need.data_ptr(), d_ws.data_ptr(), ws, long_patterns=m > 64)
+        bt = batches[state["i"] % S]
+        state["i"] += 1
+        if args.count_only:  # diagnostic: the search alone (k_count)
+            ix.count_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, d_cnt.data_ptr(),
+                                 stream=bt["stream"].cuda_stream, long_patterns=m > 64)
+            return
+        ix.locate_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, bt["loff"].data_ptr(),
+                              bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
+                              stream=bt["stream"].cuda_stream, long_patterns=m > 64)
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, S)):
         step()
-    ix.sync()
-    need = int(d_need.item())
-    if need > cap:
-        raise SystemExit(f"location buffer too small: {need} > {cap}")
+    torch.cuda.synchronize()
+    for bt in batches:
+        ix.sync(bt["stream"].cuda_stream)
+        need = int(bt["need"].item())
+        if need > cap:
+            raise SystemExit(f"location buffer too small: {need} > {cap}")
 
     # ---- timed region ------------------------------------------------------
     ix.timing_read()          # drain warmup events
-    ix.timing_enable(True)
+    ix.timing_enable(not args.no_kernel_timing, every=args.event_every)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -231,8 +264,11 @@ def main():
     if world > 1:
         elapsed = D.max_over_ranks(elapsed, device=dev)
 
+    for bt in batches:
+        ix.sync(bt["stream"].cuda_stream)
     if os.environ.get("FMX_STAMPS_OUT"):
         phase_stamps(pkg, ix, step, B, os.environ["FMX_STAMPS_OUT"])
+        torch.cuda.synchronize()
 
     # ---- result concatenation across ranks (RCCL all-gathers, untimed) -----
     gather_ms = None
@@ -257,7 +293,12 @@ def main():
     per_pattern = m + 2 * P + L * 2 * (P + BLK) + P
     per_occ = (sr - 1) * (P + BLK) + 2 * P
     kern = {name: t["total_ms"] / max(t["launches"], 1) for name, t in timing.items()}
+    if "locate" not in kern:  # --no-kernel-timing
+        kern["locate"] = float("nan")
     dominant = "locate"   # the single fused launch of a step (k_locate)
+    if args.count_only:
+        dominant = "count"
+        kern.pop("locate", None)
     alg_bytes = per_pattern * B + per_occ * total_occ
     achieved = alg_bytes / (kern[dominant] * 1e-3) / 1e9
     traffic, traffic_src = None, None
@@ -273,15 +314,19 @@ def main():
         except Exception:
             pass
 
-    # size-independent property at full size: pattern i was cut at starts[i],
-    # so starts[i] must be one of its locations
+    # size-independent property at full size, every batch: pattern i was cut
+    # at starts[i], so starts[i] must be one of its locations
+    self_found = True
+    for bt in batches:
+        bo = bt["loff"].cpu().numpy().view(np.uint64)
+        bl = bt["locs"][:int(bo[-1])].cpu().numpy().view(pdt_np)
+        st_h = bt["starts"].cpu().numpy()
+        cnt_h = np.diff(bo).astype(np.int64)
+        owner = np.repeat(np.arange(B), cnt_h)
+        hit = np.zeros(B, dtype=bool)
+        hit[owner[bl.astype(np.int64) == st_h[owner]]] = True
+        self_found = self_found and bool(hit.all() and (cnt_h >= 1).all())
     locs_h = d_locs[:total_occ].cpu().numpy().view(pdt_np)
-    st_h = starts.cpu().numpy()
-    cnt_h = np.diff(offs_h).astype(np.int64)
-    owner = np.repeat(np.arange(B), cnt_h)
-    hit = np.zeros(B, dtype=bool)
-    hit[owner[locs_h.astype(np.int64) == st_h[owner]]] = True
-    self_found = bool(hit.all() and (cnt_h >= 1).all())
 
     b_all = torch.tensor([B], dtype=torch.int64, device=dev)
     if world > 1:
@@ -310,6 +355,7 @@ def main():
             "load_options": info["options"], "deep_lut_k": info["deep_lut_k"],
             "index_hbm_bytes": info["device_bytes"],
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
+            "streams": S,
         },
         "roofline": {
             "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

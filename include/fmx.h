@@ -186,8 +186,10 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
 fmx_status fmx_sync(fmx_index *ix, void *stream);
 
 /* --------------------------------------------------------------- timing
- * When enabled, every kernel launch is bracketed by hipEvents on its stream;
- * fmx_timing_read sums their durations per kernel (it synchronises). */
+ * enable = k > 0: every k-th kernel launch (k = 1: every launch) is bracketed
+ * by hipEvents on its stream; 0: off.  fmx_timing_read sums the bracketed
+ * durations per kernel (it synchronises).  An event pair costs the stream
+ * several microseconds, so throughput runs sample (k > 1). */
 fmx_status fmx_timing_enable(fmx_index *ix, int enable);
 fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entries, int *n_entries);
 

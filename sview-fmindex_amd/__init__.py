@@ -521,8 +521,9 @@ class FmIndex:
     def sync(self, stream: int = 0) -> None:
         _check(_n.lib().fmx_sync(self._h, C.c_void_p(stream) if stream else None))
 
-    def timing_enable(self, on: bool = True) -> None:
-        _check(_n.lib().fmx_timing_enable(self._h, 1 if on else 0))
+    def timing_enable(self, on: bool = True, every: int = 1) -> None:
+        """Bracket every `every`-th launch with HIP events (fmx_timing_enable)."""
+        _check(_n.lib().fmx_timing_enable(self._h, max(1, int(every)) if on else 0))
 
     def timing_read(self) -> dict:
         arr = (_n.fmx_kernel_timing * 16)()

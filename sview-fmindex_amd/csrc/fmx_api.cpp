@@ -189,7 +189,7 @@ static Timer &timer(fmx_index *ix, const char *name) {
 // Bracket one launch with events on its stream when timing is on.
 template <class F>
 static hipError_t timed(fmx_index *ix, const char *name, hipStream_t s, uint64_t units, F &&launch) {
-    if (!ix->timing) return launch();
+    if (!ix->timing || (ix->timing_seq++ % ix->timing_every) != 0) return launch();
     hipEvent_t a = take_event(ix), b = take_event(ix);
     if (!a || !b) return hipErrorOutOfMemory;
     hipEventRecord(a, s);
@@ -254,6 +254,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         }
     }
     ix->options = ix->occ_mode;
+    if (const char *env = getenv("FMX_LOCATE_SPLIT")) ix->locate_fused = atoi(env) == 0;
     // deep-table digits: the symbols that occur in the text (a pattern holding
     // any other symbol is left to the blob's seed and the LF loop)
     uint32_t S = 0;
@@ -488,12 +489,15 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
     }));
 }
 
-// Locate workspace: [ctl: 2 x u32, padded to 256 B][tiles: 2 x tiles_cap x u64].
-static uint64_t ws_bytes_for(uint64_t n) { return 256 + 2 * locate_tiles_cap(n) * 8; }
+// Locate workspace: [ctl: 2 x u32, padded to 256 B][tiles: 2 x tiles_cap x u64]
+// [search records: n x locate_rec_bytes(P)].
+static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) {
+    return 256 + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes);
+}
 
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {
     if (!ix || !bytes) return FMX_E_ARG;
-    *bytes = ws_bytes_for(n);
+    *bytes = ws_bytes_for(ix, n);
     return FMX_OK;
 }
 
@@ -508,8 +512,11 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
         if (e == hipSuccess) e = hipMemsetAsync(d_needed, 0, 8, s);
         return dev_err(e);
     }
-    const uint64_t tiles_cap = (ws_bytes - 256) / 16;
-    if (tiles_cap < locate_tiles_cap(n)) return FMX_E_ARG;
+    if (ws_bytes < ws_bytes_for(ix, n)) return FMX_E_ARG;
+    // the fused kernel double-buffers its tile words over the whole workspace
+    // (the same split for every launch on it); the split kernels need none
+    const uint64_t tiles_cap = ix->locate_fused ? std::min<uint64_t>((ws_bytes - 256) / 16, 0xFFFFFFFFull)
+                                                : locate_tiles_cap(n);
     uint8_t *ws = (uint8_t *)d_ws;
     return dev_err(timed(ix, "locate", s, n, [&] {
         return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
@@ -559,7 +566,7 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
 
 // The host-API locate workspace lives in the index, zeroed when (re)allocated.
 static fmx_status ensure_ws(fmx_index *ix, uint64_t n) {
-    const uint64_t need = ws_bytes_for(n);
+    const uint64_t need = ws_bytes_for(ix, n);
     if (ix->ws_bytes >= need) return FMX_OK;
     if (ix->d_ws) hipFree(ix->d_ws);
     ix->d_ws = nullptr;
@@ -631,7 +638,10 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
 
 fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
     if (!ix) return FMX_E_ARG;
+    if (enable < 0) return FMX_E_ARG;
     ix->timing = enable != 0;
+    ix->timing_every = enable > 0 ? (uint32_t)enable : 1u;
+    ix->timing_seq = 0;
     return FMX_OK;
 }
 

@@ -120,6 +120,7 @@ struct fmx_index {
     uint64_t safull_bytes = 0;
     uint8_t *d_text = nullptr;
     uint32_t options = 0;
+    bool locate_fused = true;  // FMX_LOCATE_SPLIT=1: k_search + k_emit instead of k_locate (A/B)
     fmx::QueryArgs qa{};
     // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
@@ -128,6 +129,8 @@ struct fmx_index {
     uint64_t ws_bytes = 0;
     // timing
     bool timing = false;
+    uint32_t timing_every = 1;   // bracket every k-th launch
+    uint64_t timing_seq = 0;
     std::vector<fmx::Timer> timers;
     std::vector<hipEvent_t> event_pool;
     std::mutex mu;
@@ -138,14 +141,17 @@ namespace fmx {
 // Query launchers (fmx_query.hip).  All asynchronous on `stream`.
 hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                         uint32_t flags, void *d_counts, hipStream_t stream);
-// Fused count + offsets scan + locate.  d_ctl (2 x u32) and d_tiles
-// (2 x tiles_cap x u64) must be zero before their first use; the kernel keeps
+// Count + offsets scan + locate: the fused k_locate (or k_search then k_emit
+// with FMX_LOCATE_SPLIT=1).  d_ctl (2 x u32) and d_tiles (2 x tiles_cap x u64,
+// then n search records) must be zero before their first use; the kernels keep
 // them consistent across launches on one stream.
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                          uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
                          uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
                          hipStream_t stream);
 uint64_t locate_tiles_cap(uint64_t n);
+// Bytes per pattern of the search-result records in the locate workspace.
+uint64_t locate_rec_bytes(uint32_t pos_bytes);
 hipError_t launch_relayout(fmx_index *ix, hipStream_t stream);
 // Build the deep k-mer table (FMX_OPT_DEEP_LUT) for K into ix->d_dlut.
 hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream);

@@ -170,6 +170,50 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
 
 // ---------------------------------------------------------------- k_locate
 
+// The locations of a wave's 64 patterns (lane j: pattern with output slots
+// [my_off, my_off + cnt) and its search result), every occurrence row dealt
+// to the next free lane so that skewed counts keep the wave busy
+// (write_locations_to_buffer, src/locate/mod.rs:14-37): lane t of a round
+// finds its pattern by a binary search over the lanes' first slots.
+template <typename P, int N, int VB, int REC>
+__device__ __forceinline__ void emit_locations(const QueryArgs &a, const P *C, uint64_t my_off, uint64_t cnt, P lo,
+                                               P rloc, uint64_t mask, uint32_t mode, uint64_t cap,
+                                               P *__restrict__ out_locs) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t w_start = __shfl(my_off, 0);
+    const uint64_t w_end = __shfl(my_off + cnt, 63);
+    for (uint64_t t0 = w_start; t0 < w_end; t0 += 64) {
+        const uint64_t t = t0 + lane;
+        int jl = 0;  // largest lane whose first slot is <= t
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint64_t o = __shfl(my_off, jl + step);
+            if (o <= t) jl += step;
+        }
+        const P lo_j = __shfl(lo, jl);
+        const uint64_t off_j = __shfl(my_off, jl);
+        const P rloc_j = __shfl(rloc, jl);
+        const uint32_t mode_j = (uint32_t)__shfl((int)mode, jl);
+        const uint64_t mask_j = __shfl(mask, jl);
+        if (t < w_end) {
+            const uint64_t q = t - off_j;  // occurrence q of pattern jl
+            P loc;
+            if (mode_j == kHitOne) {
+                loc = rloc_j;  // resolved against the text: its one location
+            } else if (mode_j == kHitMask) {
+                uint64_t mk = mask_j;  // the q-th matching row of a scanned interval
+                for (uint64_t u = 0; u < q; ++u) mk &= mk - 1;
+                const P row = lo_j + (P)__builtin_ctzll(mk);
+                loc = reinterpret_cast<const P *>(a.safull)[(uint64_t)row * a.sa_stride] - rloc_j;
+            } else {
+                loc = walk_row<P, N, VB, REC>(a, C, lo_j + (P)q);
+            }
+            if (t < cap) out_locs[t] = loc;
+        }
+    }
+}
+
+
 // Look-back tile word: (inclusive-or-aggregate sum << 2) | flag.
 constexpr uint64_t kTileAgg = 1, kTileInc = 2;
 
@@ -250,9 +294,22 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
                 const uint64_t zerom = __ballot((w & 3) == 0);
                 const int first_inc = incm ? __builtin_ctzll(incm) : 64;
                 const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
-                if (zerom & upto) {  // a predecessor has not published yet
-                    if (++spins > (1u << 24)) { atomicOr(a.status, kStatusHang); break; }
-                    __builtin_amdgcn_s_sleep(1);
+                if (zerom & upto) {
+                    // A predecessor has not published yet (it is still
+                    // searching).  Wait on that one word from one lane — a
+                    // 64-lane window re-read per round trip from every waiting
+                    // workgroup would take a large share of the chip's memory
+                    // requests — then read the window again.
+                    const int64_t widx = j - (int64_t)__builtin_ctzll(zerom & upto);
+                    uint64_t wv = 0;
+                    bool hang = false;
+                    do {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (lane == 0) wv = __hip_atomic_load(&cur[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        wv = __shfl(wv, 0);
+                        hang = ++spins > (1u << 24);
+                    } while ((wv & 3) == 0 && !hang);
+                    if (hang) { if (lane == 0) atomicOr(a.status, kStatusHang); break; }
                     continue;
                 }
                 uint64_t v = lane <= first_inc ? (w >> 2) : 0;
@@ -279,38 +336,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     }
 
     // ---- 3. locate walk, rows of the wave's 64 patterns dealt to its lanes --
-    const int lane = threadIdx.x & 63;
-    const uint64_t w_start = __shfl(my_off, 0);
-    const uint64_t w_end = __shfl(my_off + cnt, 63);
-    for (uint64_t t0 = w_start; t0 < w_end; t0 += 64) {
-        const uint64_t t = t0 + lane;
-        int jl = 0;  // largest lane whose first slot is <= t
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const uint64_t o = __shfl(my_off, jl + step);
-            if (o <= t) jl += step;
-        }
-        const P lo_j = __shfl(lo, jl);
-        const uint64_t off_j = __shfl(my_off, jl);
-        const P rloc_j = __shfl(rloc, jl);
-        const uint32_t mode_j = (uint32_t)__shfl((int)mode, jl);
-        const uint64_t mask_j = __shfl(mask, jl);
-        if (t < w_end) {
-            const uint64_t q = t - off_j;  // occurrence q of pattern jl
-            P loc;
-            if (mode_j == kHitOne) {
-                loc = rloc_j;  // resolved against the text: its one location
-            } else if (mode_j == kHitMask) {
-                uint64_t mk = mask_j;  // the q-th matching row of a scanned interval
-                for (uint64_t u = 0; u < q; ++u) mk &= mk - 1;
-                const P row = lo_j + (P)__builtin_ctzll(mk);
-                loc = reinterpret_cast<const P *>(a.safull)[(uint64_t)row * a.sa_stride] - rloc_j;
-            } else {
-                loc = walk_row<P, N, VB, REC>(a, s.C, lo_j + (P)q);
-            }
-            if (t < cap) out_locs[t] = loc;
-        }
-    }
+    emit_locations<P, N, VB, REC>(a, s.C, my_off, cnt, lo, rloc, mask, mode, cap, out_locs);
 #ifdef FMX_PHASE_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
 #endif
@@ -324,6 +350,133 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
             __hip_atomic_store(&ctl[1], s_par ^ 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// ------------------------------------------------- k_search + k_emit (split)
+
+// A pattern's search result, handed from k_search to k_emit (P-typed words):
+//   rows (kHitRows): a = lo,   b = count, x = 0
+//   one  (kHitOne):  a = rloc, b = count, x = 1
+//   mask (kHitMask): a = lo,   b = rloc,  x = mask (>= 2 bits set, count = popcount)
+template <typename P>
+struct SearchRec {
+    P a, b;
+    uint64_t x;
+};
+
+template <typename P>
+__device__ __forceinline__ SearchRec<P> pack_rec(P lo, P hi, P rloc, uint64_t mask, uint32_t mode) {
+    if (mode == kHitOne) return {rloc, (P)(hi - lo), 1ull};
+    if (mode == kHitMask) return {lo, rloc, mask};
+    return {lo, (P)(hi - lo), 0ull};
+}
+
+template <typename P>
+__device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &rloc, uint64_t &mask,
+                                               uint32_t &mode) {
+    // Selects, not branches: the if-chain form of this decode was miscompiled
+    // (hipcc 7.2, gfx950: lo/rloc left undefined on the x > 1 path).
+    const uint64_t x = r.x;
+    const bool is_one = x == 1, is_mask = x > 1;
+    mode = is_mask ? kHitMask : (is_one ? kHitOne : kHitRows);
+    lo = is_one ? P(0) : r.a;
+    rloc = is_mask ? r.b : (is_one ? r.a : P(0));
+    mask = is_mask ? x : 0ull;
+    return is_mask ? (uint64_t)__builtin_popcountll(x) : (uint64_t)r.b;
+}
+
+// Phase 1 of a locate batch: the search of every pattern (no waiting on other
+// workgroups), its result record, and the tile's count.  The last workgroup
+// to finish (agent-scope counter) turns the tile counts into exclusive tile
+// offsets and the batch total, so k_emit needs no look-back.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_search(const QueryArgs a, const uint8_t *__restrict__ bytes,
+                                                const uint64_t *__restrict__ offs, uint64_t npat, uint32_t flags,
+                                                P *__restrict__ out_cnt, SearchRec<P> *__restrict__ recs,
+                                                uint64_t *__restrict__ tile_cnt, uint64_t *__restrict__ tile_off,
+                                                uint32_t *__restrict__ ctl, uint64_t *__restrict__ loc_off,
+                                                uint64_t *__restrict__ needed, uint32_t stage_bytes) {
+    __shared__ Tables<P> s;
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
+    __shared__ uint64_t s_scan[4];
+    __shared__ uint32_t s_last;
+    stage_tables(a, s);
+    const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
+    const uint32_t G = (uint32_t)((npat + 255) / 256), g = blockIdx.x;
+    uint64_t beg, end, b0, b1;
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end,
+                                       b0, b1);
+    __syncthreads();
+    const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
+    uint64_t cnt = 0;
+    if (i < npat) {
+        const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
+        P lo, hi, rloc;
+        uint64_t mask;
+        uint32_t mode;
+        const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
+        if (bad) atomicOr(a.status, bad);
+        cnt = (uint64_t)(hi - lo);
+        if (out_cnt) out_cnt[i] = hi - lo;
+        recs[i] = pack_rec<P>(lo, hi, rloc, mask, mode);
+    }
+    uint64_t agg;
+    block_excl_scan(cnt, &agg, s_scan);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&tile_cnt[g], agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t done = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = done == G - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // The last workgroup: exclusive scan of the G tile counts, 16 per thread
+    // per pass (every load of a pass in flight at once).
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < G; base += 256 * 16) {
+        uint64_t v[16], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint64_t t = base + threadIdx.x * 16ull + u;
+            v[u] = t < G ? __hip_atomic_load(&tile_cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            sum += v[u];
+        }
+        uint64_t tot;
+        uint64_t run = carry + block_excl_scan(sum, &tot, s_scan);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint64_t t = base + threadIdx.x * 16ull + u;
+            if (t < G) tile_off[t] = run;
+            run += v[u];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        loc_off[npat] = carry;
+        *needed = carry;
+        __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+    }
+}
+
+// Phase 2: output offsets (tile offset + in-tile scan) and every location,
+// rows dealt across each wave's lanes (emit_locations).
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_emit(const QueryArgs a, uint64_t npat, const SearchRec<P> *__restrict__ recs,
+                                              const uint64_t *__restrict__ tile_off, uint64_t *__restrict__ loc_off,
+                                              P *__restrict__ out_locs, uint64_t cap) {
+    __shared__ P sC[kMaxSigma + 1];
+    __shared__ uint64_t s_scan[4];
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
+    const uint64_t g = blockIdx.x, i = g * 256u + threadIdx.x;
+    P lo = 0, rloc = 0;
+    uint64_t mask = 0, cnt = 0;
+    uint32_t mode = kHitOne;
+    if (i < npat) cnt = unpack_rec<P>(recs[i], lo, rloc, mask, mode);
+    const uint64_t base = tile_off[g];
+    uint64_t agg;
+    const uint64_t my_off = base + block_excl_scan(cnt, &agg, s_scan);  // (its barriers publish sC)
+    if (i < npat) loc_off[i] = my_off;
+    emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, cap, out_locs);
 }
 
 // ------------------------------------------------------------ deep k-mer table
@@ -532,11 +685,26 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
     if ((n + 255) / 256 > tiles_cap || tiles_cap > 0xFFFFFFFFull) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         const uint32_t sb = stage_bytes_for(flags);
-        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
-                           d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed, d_ctl,
-                           d_tiles, (uint32_t)tiles_cap, sb);
+        if (ix->locate_fused) {
+            hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
+                               d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed, d_ctl,
+                               d_tiles, (uint32_t)tiles_cap, sb);
+            return hipGetLastError();
+        }
+        // workspace: [tile counts: tiles_cap][tile offsets: tiles_cap][records: n]
+        uint64_t *tile_cnt = d_tiles, *tile_off = d_tiles + tiles_cap;
+        SearchRec<P> *recs = reinterpret_cast<SearchRec<P> *>(d_tiles + 2 * tiles_cap);
+        hipLaunchKernelGGL((k_search<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
+                           d_offsets, n, flags, (P *)d_counts, recs, tile_cnt, tile_off, d_ctl, d_loc_offsets,
+                           d_needed, sb);
+        hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, n,
+                           (const SearchRec<P> *)recs, (const uint64_t *)tile_off, d_loc_offsets, (P *)d_locs, cap);
         return hipGetLastError();
     });
+}
+
+uint64_t locate_rec_bytes(uint32_t pos_bytes) {
+    return pos_bytes == 4 ? sizeof(SearchRec<uint32_t>) : sizeof(SearchRec<uint64_t>);
 }
 
 hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream) {
