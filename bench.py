@@ -123,6 +123,11 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight: step i runs batch i %% S on HIP stream i %% S (each stream its own "
                          "patterns, outputs and look-back workspace), as a serving loop pipelines batches")
+    ap.add_argument("--batches", type=int, default=8,
+                    help="distinct pattern batches cycled over the steps (at least --streams)")
+    ap.add_argument("--submit", default="native", choices=["native", "python"],
+                    help="native: the timed steps are issued as one fmx_locate_jobs_async queue; "
+                         "python: one fmx_locate_batch_async call per step")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_fetch_size.json"))
     return ap.parse_args()
 
@@ -199,18 +204,23 @@ def main():
     log(f"[rank {rank}] index loaded in {load_s:.2f}s: options={info['options']} deep_lut_k={info['deep_lut_k']} "
         f"device_bytes={info['device_bytes']:,}")
 
-    # ---- patterns: substrings at uniform starts (per-rank, per-stream seed) --
-    # One batch per stream; batch 0 is the one checked against the CPU oracle.
+    # ---- patterns: substrings at uniform starts (per-rank, per-batch seed) ---
+    # NB distinct batches (each its own patterns, outputs and look-back
+    # workspace), batch b always on stream b % S; step i runs batch i % NB, so
+    # consecutive passes over one batch are NB steps apart (their index lines
+    # are not still cached).  Batch 0 is the one checked against the CPU oracle.
     S = max(1, args.streams)
+    NB = max(S, args.batches)
     cap = 4 * B + 4096
     ws = ix.locate_workspace_size(B)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     batches = []
-    for si in range(S):
+    for bi in range(NB):
         pg = torch.Generator(device=dev)
-        pg.manual_seed(args.seed * 1000 + 7 + rank + 100003 * si)
+        pg.manual_seed(args.seed * 1000 + 7 + rank + 100003 * bi)
         starts = torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg)
         batches.append(dict(
-            stream=torch.cuda.Stream(device=dev),
+            stream=streams[bi % S],
             starts=starts,
             pat=d_text[(starts[:, None] + torch.arange(m, device=dev)[None, :]).reshape(-1)].contiguous(),
             off=(torch.arange(B + 1, device=dev, dtype=torch.int64) * m).contiguous(),
@@ -225,8 +235,13 @@ def main():
 
     d_cnt = torch.zeros(B, dtype=pdt_t, device=dev)
 
+    def job(bt):
+        return ix.locate_job(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, bt["loff"].data_ptr(),
+                             bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
+                             stream=bt["stream"].cuda_stream, long_patterns=m > 64)
+
     def step():
-        bt = batches[state["i"] % S]
+        bt = batches[state["i"] % NB]
         state["i"] += 1
         if args.count_only:  # diagnostic: the search alone (k_count)
             ix.count_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, d_cnt.data_ptr(),
@@ -236,7 +251,12 @@ def main():
                               bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
                               stream=bt["stream"].cuda_stream, long_patterns=m > 64)
 
-    for _ in range(max(args.warmup, S)):
+    # native submission: the K steps of the timed region as one queue of K
+    # jobs (step i = batch i % NB), issued by one fmx_locate_jobs_async call
+    native = args.submit == "native" and not args.count_only
+    queue = ix.job_queue([job(batches[i % NB]) for i in range(args.steps)]) if native else None
+
+    for _ in range(max(args.warmup, NB)):
         step()
     torch.cuda.synchronize()
     for bt in batches:
@@ -244,6 +264,7 @@ def main():
         need = int(bt["need"].item())
         if need > cap:
             raise SystemExit(f"location buffer too small: {need} > {cap}")
+    state["i"] = 0
 
     # ---- timed region ------------------------------------------------------
     ix.timing_read()          # drain warmup events
@@ -252,8 +273,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if native:
+        ix.locate_jobs_async(queue)
+    else:
+        for _ in range(args.steps):
+            step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:
@@ -355,7 +379,7 @@ def main():
             "load_options": info["options"], "deep_lut_k": info["deep_lut_k"],
             "index_hbm_bytes": info["device_bytes"],
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
-            "streams": S,
+            "streams": S, "distinct_batches": NB, "submit": "native" if native else "python",
         },
         "roofline": {
             "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -140,6 +140,18 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
                            uint32_t options, fmx_index **out, uint64_t *expected_total,
                            uint64_t *actual_total);
 
+/* Blob ingest from a file (the bench's mmap / read-whole-file loaders,
+ * bench/src/locate/sview_mmap.rs:17-45 and sview_memory.rs:17-20, then
+ * FmIndex::load).  The header is read and validated first (same checks and
+ * codes as fmx_load; the file size is the blob length); the body is then
+ * streamed file -> pinned host chunks -> HBM, reads overlapping the DMA of
+ * the previous chunk, so no host copy of the whole blob is ever held.
+ * chunk_bytes = 0 picks the default (64 MiB).  FMX_E_ARG if the file cannot
+ * be opened or read.  fmx_blob() returns NULL for such an index. */
+fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32_t options,
+                         uint64_t chunk_bytes, fmx_index **out, uint64_t *expected_total,
+                         uint64_t *actual_total);
+
 void fmx_free(fmx_index *ix);
 
 /* FmIndex::blob (src/reference_to_source_blob.rs:9-11).  NULL for device loads. */
@@ -181,6 +193,28 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
                                   uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
                                   uint64_t *d_needed, void *d_workspace, uint64_t workspace_bytes,
                                   void *stream);
+
+/* A queue of locate batches submitted in one call (a serving loop's batches
+ * in flight): job i is exactly fmx_locate_batch_async(ix, jobs[i].d_bytes,
+ * ...), issued in order, each on its own stream; the call returns after the
+ * last launch is queued (or at the first error, which it returns). */
+typedef struct fmx_locate_job {
+    const uint8_t *d_bytes;
+    const uint64_t *d_offsets;
+    uint64_t n_patterns;
+    uint32_t flags;
+    uint32_t reserved;         /* 0 */
+    void *d_counts;            /* optional */
+    uint64_t *d_loc_offsets;
+    void *d_locs;
+    uint64_t cap;
+    uint64_t *d_needed;
+    void *d_workspace;
+    uint64_t workspace_bytes;
+    void *stream;              /* hipStream_t; NULL = the index's own stream */
+} fmx_locate_job;
+
+fmx_status fmx_locate_jobs_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs);
 
 /* Wait for `stream` and return (and clear) the latched device status. */
 fmx_status fmx_sync(fmx_index *ix, void *stream);

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${TAG:-r1}
 ARGS=${BENCH_ARGS:-"--steps 50 --warmup 5 --no-cpu"}
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/${T}_build.log 2>&1 &&
+# (the engine is built here, in-tree, before the call; the box only runs it)
 timeout -k 10 120 rocprofv3 -L > gpurun_out/${T}_counters.txt 2>&1;
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${T}_trace.log 2>&1 && echo trace-ok &&
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${T}_pmc1 -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/${T}_pmc1.log 2>&1 && echo pmc1-ok &&

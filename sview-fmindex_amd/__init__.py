@@ -28,6 +28,7 @@ CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -401,6 +402,34 @@ class FmIndex:
         _check(st, "fmx_load_device")
         return cls(h, position, block, text_encoder, None)
 
+    @classmethod
+    def load_file(cls, path, position: Position = u32, block: Optional[_Block] = None,
+                  text_encoder=text_encoders.EncodingTable, device: int = 0, occ: str = "interleaved",
+                  deep_lut: bool = True, full_sa: bool = True, text: bool = True, context: bool = True,
+                  lut_rows: bool = True, options: Optional[int] = None, chunk_bytes: int = 0) -> "FmIndex":
+        """Blob file -> HBM (fmx_load_file): what the bench's mmap loader
+        (bench/src/locate/sview_mmap.rs:17-45) followed by ``FmIndex::load``
+        does, as a streamed ingest — the header is validated from the file,
+        then the body is read in pinned chunks overlapped with their DMA."""
+        block = block or blocks.Block2(Vector.U64)
+        if isinstance(text_encoder, type):
+            text_encoder = text_encoder.__new__(text_encoder)
+        h = C.c_void_p()
+        exp, act = C.c_uint64(), C.c_uint64()
+        mode = options if options is not None else _options(occ, deep_lut, full_sa, text, context, lut_rows)
+        st = _n.lib().fmx_load_file(os.fsencode(path), _layout(position, block, text_encoder), device, mode,
+                                    int(chunk_bytes), C.byref(h), C.byref(exp), C.byref(act))
+        if st == _n.FMX_E_FORMAT:
+            raise InvalidFormat()
+        if st == _n.FMX_E_SIZE:
+            raise MismatchedBlobSize(exp.value, act.value)
+        _check(st, f"fmx_load_file({path})")
+        if isinstance(text_encoder, text_encoders.EncodingTable) and not hasattr(text_encoder, "table"):
+            with open(path, "rb") as f:
+                f.seek(8 if block.ALIGN_SIZE == 8 else 16)
+                text_encoder.table = f.read(256)
+        return cls(h, position, block, text_encoder, None)
+
     def close(self):
         if self._h:
             _n.lib().fmx_free(self._h)
@@ -517,6 +546,26 @@ class FmIndex:
             C.c_void_p(d_counts) if d_counts else None, C.c_void_p(d_loc_offsets), C.c_void_p(d_locs), cap,
             C.c_void_p(d_needed) if d_needed else None, C.c_void_p(d_ws), ws_bytes,
             C.c_void_p(stream) if stream else None))
+
+    @staticmethod
+    def locate_job(d_bytes: int, d_offsets: int, n: int, d_loc_offsets: int, d_locs: int, cap: int,
+                   d_needed: int, d_ws: int, ws_bytes: int, d_counts: int = 0, stream: int = 0,
+                   reversed: bool = False, long_patterns: bool = False) -> "_n.fmx_locate_job":
+        """One entry of a locate queue (fmx_locate_job): the arguments of
+        locate_batch_async."""
+        flags = (_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
+        return _n.fmx_locate_job(d_bytes, d_offsets, n, flags, 0, d_counts or None, d_loc_offsets, d_locs, cap,
+                                 d_needed, d_ws, ws_bytes, stream or None)
+
+    @staticmethod
+    def job_queue(jobs) -> "C.Array":
+        """A ctypes array of jobs, built once and submitted many times."""
+        return (_n.fmx_locate_job * len(jobs))(*jobs)
+
+    def locate_jobs_async(self, queue) -> None:
+        """Issue a queue of locate batches in one native call
+        (fmx_locate_jobs_async): no per-batch Python overhead."""
+        _check(_n.lib().fmx_locate_jobs_async(self._h, queue, len(queue)))
 
     def sync(self, stream: int = 0) -> None:
         _check(_n.lib().fmx_sync(self._h, C.c_void_p(stream) if stream else None))

@@ -53,6 +53,14 @@ class fmx_index_info(C.Structure):
                 ("context_len", C.c_uint32), ("scan_rows", C.c_uint32)]
 
 
+class fmx_locate_job(C.Structure):
+    _fields_ = [("d_bytes", C.c_void_p), ("d_offsets", C.c_void_p), ("n_patterns", C.c_uint64),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32), ("d_counts", C.c_void_p),
+                ("d_loc_offsets", C.c_void_p), ("d_locs", C.c_void_p), ("cap", C.c_uint64),
+                ("d_needed", C.c_void_p), ("d_workspace", C.c_void_p), ("workspace_bytes", C.c_uint64),
+                ("stream", C.c_void_p)]
+
+
 class fmx_kernel_timing(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64),
                 ("total_ms", C.c_double), ("units", C.c_uint64)]
@@ -68,6 +76,7 @@ SIGNATURES = {
     "fmx_device_count": (_i, []),
     "fmx_load": (_i, [_p, _u64, fmx_layout, _i, _u32, C.POINTER(_p), _PU64, _PU64]),
     "fmx_load_device": (_i, [_p, _u64, fmx_layout, _i, _u32, C.POINTER(_p), _PU64, _PU64]),
+    "fmx_load_file": (_i, [C.c_char_p, fmx_layout, _i, _u32, _u64, C.POINTER(_p), _PU64, _PU64]),
     "fmx_free": (None, [_p]),
     "fmx_blob": (_p, [_p, _PU64]),
     "fmx_info": (_i, [_p, C.POINTER(fmx_index_info)]),
@@ -76,6 +85,7 @@ SIGNATURES = {
     "fmx_count_batch_async": (_i, [_p, _p, _p, _u64, _u32, _p, _p]),
     "fmx_locate_workspace_size": (_i, [_p, _u64, _PU64]),
     "fmx_locate_batch_async": (_i, [_p, _p, _p, _u64, _u32, _p, _p, _p, _u64, _p, _p, _u64, _p]),
+    "fmx_locate_jobs_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64]),
     "fmx_sync": (_i, [_p, _p]),
     "fmx_timing_enable": (_i, [_p, _i]),
     "fmx_timing_read": (_i, [_p, C.POINTER(fmx_kernel_timing), _i, C.POINTER(_i)]),

@@ -2,6 +2,10 @@
 // batch orchestration, timing.  Host side of the MI355X engine.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -433,6 +437,88 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
     return FMX_OK;
 }
 
+// Streamed file ingest: pread into two pinned chunks, each handed to the DMA
+// engine as soon as it is full; the read of chunk i+1 overlaps the copy of
+// chunk i (the event of a chunk's previous copy gates its reuse).
+static bool read_full(int fd, uint64_t off, uint64_t len, void *dst) {
+    uint8_t *d = (uint8_t *)dst;
+    while (len) {
+        const ssize_t r = pread(fd, d, len > (1ull << 30) ? (1ull << 30) : len, (off_t)off);
+        if (r <= 0) return false;
+        d += r;
+        off += (uint64_t)r;
+        len -= (uint64_t)r;
+    }
+    return true;
+}
+
+static fmx_status stream_file(int fd, uint64_t len, uint8_t *d_dst, uint64_t chunk) {
+    hipStream_t s = nullptr;
+    void *buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    fmx_status st = FMX_OK;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
+    for (int b = 0; b < 2 && st == FMX_OK; ++b)
+        if (hipHostMalloc(&buf[b], chunk, hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[b], hipEventDisableTiming) != hipSuccess)
+            st = FMX_E_DEVICE;
+    bool used[2] = {false, false};
+    for (uint64_t off = 0, i = 0; st == FMX_OK && off < len; off += chunk, ++i) {
+        const int b = (int)(i & 1);
+        const uint64_t n = std::min<uint64_t>(chunk, len - off);
+        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { st = FMX_E_DEVICE; break; }
+        if (!read_full(fd, off, n, buf[b])) { st = FMX_E_ARG; break; }
+        if (hipMemcpyAsync(d_dst + off, buf[b], n, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(ev[b], s) != hipSuccess) { st = FMX_E_DEVICE; break; }
+        used[b] = true;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && st == FMX_OK) st = FMX_E_DEVICE;
+    for (int b = 0; b < 2; ++b) {
+        if (ev[b]) hipEventDestroy(ev[b]);
+        if (buf[b]) hipHostFree(buf[b]);
+    }
+    hipStreamDestroy(s);
+    return st;
+}
+
+fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32_t options, uint64_t chunk_bytes,
+                         fmx_index **out, uint64_t *expected_total, uint64_t *actual_total) {
+    if (!out || !path) return FMX_E_ARG;
+    *out = nullptr;
+    if (!layout_valid(layout)) return FMX_E_LAYOUT;
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return FMX_E_ARG;
+    struct stat sb;
+    if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close(fd); return FMX_E_ARG; }
+    const uint64_t blob_len = (uint64_t)sb.st_size;
+    BlobView bv;
+    BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
+        return off + len <= blob_len && read_full(fd, off, len, dst);
+    };
+    fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
+    if (st) { close(fd); return st; }
+    if (hipSetDevice(device) != hipSuccess) { close(fd); return FMX_E_DEVICE; }
+    fmx_index *ix = new (std::nothrow) fmx_index();
+    if (!ix) { close(fd); return FMX_E_DEVICE; }
+    ix->bv = bv;
+    ix->device = device;
+    ix->blob_len = blob_len;
+    if (hipMalloc(&ix->d_blob_owned, std::max<uint64_t>(blob_len, 1)) != hipSuccess) {
+        close(fd);
+        fmx_free(ix);
+        return FMX_E_DEVICE;
+    }
+    const uint64_t chunk = chunk_bytes ? align_up(chunk_bytes, 4096) : (64ull << 20);
+    st = stream_file(fd, blob_len, ix->d_blob_owned, chunk);
+    close(fd);
+    if (st) { fmx_free(ix); return st; }
+    ix->d_blob = ix->d_blob_owned;
+    st = finish_load(ix, options);
+    if (st) { fmx_free(ix); return st; }
+    *out = ix;
+    return FMX_OK;
+}
+
 void fmx_free(fmx_index *ix) {
     if (!ix) return;
     hipSetDevice(ix->device);
@@ -522,6 +608,18 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
         return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
                              (uint32_t *)ws, (uint64_t *)(ws + 256), tiles_cap, s);
     }));
+}
+
+fmx_status fmx_locate_jobs_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs) {
+    if (!ix || (n_jobs && !jobs)) return FMX_E_ARG;
+    for (uint64_t i = 0; i < n_jobs; ++i) {
+        const fmx_locate_job &j = jobs[i];
+        const fmx_status st =
+            fmx_locate_batch_async(ix, j.d_bytes, j.d_offsets, j.n_patterns, j.flags, j.d_counts, j.d_loc_offsets,
+                                   j.d_locs, j.cap, j.d_needed, j.d_workspace, j.workspace_bytes, j.stream);
+        if (st) return st;
+    }
+    return FMX_OK;
 }
 
 fmx_status fmx_sync(fmx_index *ix, void *stream) {
