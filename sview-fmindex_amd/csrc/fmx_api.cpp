@@ -599,14 +599,29 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
         return dev_err(e);
     }
     if (ws_bytes < ws_bytes_for(ix, n)) return FMX_E_ARG;
-    // the fused kernel double-buffers its tile words over the whole workspace
-    // (the same split for every launch on it); the split kernels need none
-    const uint64_t tiles_cap = ix->locate_fused ? std::min<uint64_t>((ws_bytes - 256) / 16, 0xFFFFFFFFull)
-                                                : locate_tiles_cap(n);
     uint8_t *ws = (uint8_t *)d_ws;
+    const uint64_t G = locate_tiles_cap(n);
+    uint32_t epoch = 0;
+    if (ix->locate_fused) {
+        // The next look-back epoch of this workspace; after kLocateEpochs
+        // launches, the tiles any of them published are zeroed (stream-ordered
+        // before this launch) and the epochs start again.
+        uint64_t clear_tiles = 0;
+        {
+            std::lock_guard<std::mutex> g(ix->ws_mu);
+            fmx_index::WsState &w = ix->ws_state[d_ws];
+            if (w.epoch >= kLocateEpochs) {
+                clear_tiles = w.hi_tiles;
+                w.epoch = 0;
+            }
+            epoch = ++w.epoch;
+            w.hi_tiles = std::max(w.hi_tiles, G);
+        }
+        if (clear_tiles && hipMemsetAsync(ws + 256, 0, clear_tiles * 8, s) != hipSuccess) return FMX_E_DEVICE;
+    }
     return dev_err(timed(ix, "locate", s, n, [&] {
         return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
-                             (uint32_t *)ws, (uint64_t *)(ws + 256), tiles_cap, s);
+                             (uint32_t *)ws, (uint64_t *)(ws + 256), G, epoch, s);
     }));
 }
 
@@ -666,7 +681,11 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
 static fmx_status ensure_ws(fmx_index *ix, uint64_t n) {
     const uint64_t need = ws_bytes_for(ix, n);
     if (ix->ws_bytes >= need) return FMX_OK;
-    if (ix->d_ws) hipFree(ix->d_ws);
+    if (ix->d_ws) {
+        hipFree(ix->d_ws);
+        std::lock_guard<std::mutex> g(ix->ws_mu);
+        ix->ws_state.erase(ix->d_ws);
+    }
     ix->d_ws = nullptr;
     ix->ws_bytes = 0;
     const uint64_t want = std::max<uint64_t>(need, 1 << 16);

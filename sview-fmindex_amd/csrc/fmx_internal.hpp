@@ -8,6 +8,7 @@
 #include <functional>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/fmx.h"
@@ -131,6 +132,14 @@ struct fmx_index {
     bool timing = false;
     uint32_t timing_every = 1;   // bracket every k-th launch
     uint64_t timing_seq = 0;
+    // k_locate look-back state per caller workspace: the last epoch handed
+    // out, and the most tiles ever published on it (what a wrap must clear)
+    struct WsState {
+        uint32_t epoch = 0;
+        uint64_t hi_tiles = 0;
+    };
+    std::unordered_map<const void *, WsState> ws_state;
+    std::mutex ws_mu;
     std::vector<fmx::Timer> timers;
     std::vector<hipEvent_t> event_pool;
     std::mutex mu;
@@ -142,13 +151,16 @@ namespace fmx {
 hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                         uint32_t flags, void *d_counts, hipStream_t stream);
 // Count + offsets scan + locate: the fused k_locate (or k_search then k_emit
-// with FMX_LOCATE_SPLIT=1).  d_ctl (2 x u32) and d_tiles (2 x tiles_cap x u64,
-// then n search records) must be zero before their first use; the kernels keep
-// them consistent across launches on one stream.
+// with FMX_LOCATE_SPLIT=1).  d_ctl (2 x u32) and d_tiles must be zero before
+// their first use.  k_locate: d_tiles holds tiles_cap epoch-tagged look-back
+// words, epoch in 1..kLocateEpochs (fmx_api.cpp hands them out per workspace);
+// split: d_tiles = [tile counts][tile offsets][n search records], d_ctl its
+// finished-workgroup counter, reset by the kernel.
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                          uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
                          uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
-                         hipStream_t stream);
+                         uint32_t epoch, hipStream_t stream);
+constexpr uint32_t kLocateEpochs = 63;  // k_locate tile words carry 6 bits of epoch
 uint64_t locate_tiles_cap(uint64_t n);
 // Bytes per pattern of the search-result records in the locate workspace.
 uint64_t locate_rec_bytes(uint32_t pos_bytes);

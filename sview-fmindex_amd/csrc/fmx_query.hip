@@ -214,7 +214,13 @@ __device__ __forceinline__ void emit_locations(const QueryArgs &a, const P *C, u
 }
 
 
-// Look-back tile word: (inclusive-or-aggregate sum << 2) | flag.
+// Look-back tile word: (sum << 8) | (epoch << 2) | flag, sum = the tile's
+// aggregate (kTileAgg) or inclusive prefix (kTileInc).  A word whose epoch is
+// not this launch's is unpublished: the workspace needs no clearing between
+// launches, and no workgroup has to learn that it is the last one out (that
+// took one same-address device-scope atomic per workgroup, serialised across
+// the XCDs, at the tail of every launch).  The host hands out epochs
+// 1..kLocateEpochs per workspace and zeroes the used tiles before reusing 1.
 constexpr uint64_t kTileAgg = 1, kTileInc = 2;
 
 template <typename P, int N, int VB, int REC>
@@ -222,13 +228,12 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
                                                 const uint64_t *__restrict__ offs, uint64_t npat, uint32_t flags,
                                                 P *__restrict__ out_cnt, uint64_t *__restrict__ loc_off,
                                                 P *__restrict__ out_locs, uint64_t cap, uint64_t *__restrict__ needed,
-                                                uint32_t *__restrict__ ctl, uint64_t *__restrict__ tiles,
-                                                uint32_t tiles_cap, uint32_t stage_bytes) {
+                                                uint64_t *__restrict__ tiles, uint32_t epoch,
+                                                uint32_t stage_bytes) {
     __shared__ Tables<P> s;
     extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     __shared__ uint64_t s_scan[4];
     __shared__ uint64_t s_prefix;
-    __shared__ uint32_t s_par;
     FMX_STAMP(0, __builtin_amdgcn_s_memrealtime());
     stage_tables(a, s);
     const uint32_t G = (uint32_t)((npat + 255) / 256);
@@ -239,9 +244,6 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     // same at the price of 391 serialised atomics on one address before any
     // pattern is read — 5-10 us of a 30 us launch, measured.)
     const uint32_t g = blockIdx.x;
-    // Which of the two tile-status buffers this launch uses: read now, needed
-    // after the search (the last workgroup to finish flips it, see the end).
-    if (threadIdx.x == 0) s_par = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     FMX_STAMP(6, __builtin_amdgcn_s_memrealtime());
 
     // ---- 1. SA interval of every pattern of the tile ----------------------
@@ -267,52 +269,53 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
 
     // ---- 2. output offsets: single-pass scan with decoupled look-back -----
     uint64_t agg;
-    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);  // (its barriers publish s_par)
-    uint64_t *cur = tiles + (uint64_t)s_par * tiles_cap;
-    uint64_t *nxt = tiles + (uint64_t)(s_par ^ 1u) * tiles_cap;
-    // clear the other tile buffer for the next launch (this launch never reads it)
-    for (uint64_t x = (uint64_t)g * 256 + threadIdx.x; x < tiles_cap; x += (uint64_t)G * 256) nxt[x] = 0;
+    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);
+    const uint64_t ep = (uint64_t)epoch << 2;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         if (g == 0) {
             if (lane == 0) {
-                __hip_atomic_store(&cur[0], (agg << 2) | kTileInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&tiles[0], (agg << 8) | ep | kTileInc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
                 s_prefix = 0;
             }
         } else {
             if (lane == 0)
-                __hip_atomic_store(&cur[g], (agg << 2) | kTileAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&tiles[g], (agg << 8) | ep | kTileAgg, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             uint64_t prefix = 0;
             int64_t j = (int64_t)g - 1;
             uint32_t spins = 0;
             while (true) {
                 const int64_t idx = j - lane;
                 const uint64_t w = idx >= 0
-                    ? __hip_atomic_load(&cur[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : kTileInc;  // before tile 0: an inclusive prefix of 0
-                const uint64_t incm = __ballot((w & 3) == kTileInc);
-                const uint64_t zerom = __ballot((w & 3) == 0);
+                    ? __hip_atomic_load(&tiles[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : (ep | kTileInc);  // before tile 0: an inclusive prefix of 0
+                const bool live = (w & 0xFCull) == ep && (w & 3) != 0;  // published by this launch
+                const uint64_t incm = __ballot(live && (w & 3) == kTileInc);
+                const uint64_t waitm = __ballot(!live);
                 const int first_inc = incm ? __builtin_ctzll(incm) : 64;
                 const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
-                if (zerom & upto) {
+                if (waitm & upto) {
                     // A predecessor has not published yet (it is still
                     // searching).  Wait on that one word from one lane — a
                     // 64-lane window re-read per round trip from every waiting
                     // workgroup would take a large share of the chip's memory
                     // requests — then read the window again.
-                    const int64_t widx = j - (int64_t)__builtin_ctzll(zerom & upto);
+                    const int64_t widx = j - (int64_t)__builtin_ctzll(waitm & upto);
                     uint64_t wv = 0;
                     bool hang = false;
                     do {
                         __builtin_amdgcn_s_sleep(2);
-                        if (lane == 0) wv = __hip_atomic_load(&cur[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (lane == 0)
+                            wv = __hip_atomic_load(&tiles[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         wv = __shfl(wv, 0);
                         hang = ++spins > (1u << 24);
-                    } while ((wv & 3) == 0 && !hang);
+                    } while (((wv & 0xFCull) != ep || (wv & 3) == 0) && !hang);
                     if (hang) { if (lane == 0) atomicOr(a.status, kStatusHang); break; }
                     continue;
                 }
-                uint64_t v = lane <= first_inc ? (w >> 2) : 0;
+                uint64_t v = lane <= first_inc ? (w >> 8) : 0;
 #pragma unroll
                 for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
                 prefix += v;
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
                 j -= 64;
             }
             if (lane == 0) {
-                __hip_atomic_store(&cur[g], ((prefix + agg) << 2) | kTileInc, __ATOMIC_RELAXED,
+                __hip_atomic_store(&tiles[g], ((prefix + agg) << 8) | ep | kTileInc, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 s_prefix = prefix;
             }
@@ -341,15 +344,6 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t
     __builtin_amdgcn_s_waitcnt(0);
 #endif
     FMX_STAMP(4, __builtin_amdgcn_s_memrealtime());
-    // The last workgroup out flips the buffer parity for the next launch on
-    // this workspace and resets the counter (kernel boundaries publish both).
-    if (threadIdx.x == 0) {
-        const uint32_t done = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == G - 1) {
-            __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl[1], s_par ^ 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // ------------------------------------------------- k_search + k_emit (split)
@@ -680,15 +674,16 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                          uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
                          uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
-                         hipStream_t stream) {
+                         uint32_t epoch, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if ((n + 255) / 256 > tiles_cap || tiles_cap > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    if (ix->locate_fused && (epoch == 0 || epoch > kLocateEpochs)) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         const uint32_t sb = stage_bytes_for(flags);
         if (ix->locate_fused) {
             hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
-                               d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed, d_ctl,
-                               d_tiles, (uint32_t)tiles_cap, sb);
+                               d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed,
+                               d_tiles, epoch, sb);
             return hipGetLastError();
         }
         // workspace: [tile counts: tiles_cap][tile offsets: tiles_cap][records: n]

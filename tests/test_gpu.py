@@ -384,3 +384,49 @@ def test_absent_symbols_gpu(pkg, O):
                 got = ("err", e.code)
             assert got == want, (p, occ, got, want)
         ix.close()
+
+
+def test_locate_queue_many_launches_one_workspace(pkg, O):
+    """200 launches of varying batch sizes on one workspace, issued as one
+    fmx_locate_jobs_async queue (the look-back epochs of a workspace wrap
+    every 63 launches and its tiles are cleared then): every launch's results
+    equal the host API's, batches of different sizes interleaved."""
+    import torch
+    rng = np.random.default_rng(21)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=100_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    dev = torch.device("cuda:0")
+    sizes = [3000, 700, 1, 2049]
+    bats = []
+    for n in sizes:
+        starts = rng.integers(0, text.size - 12, size=n)
+        pats = [text[s:s + int(rng.integers(1, 13))].tobytes() for s in starts]
+        data, offsets = pkg.pack_patterns(pats)
+        want = ix.locate_batch((data, offsets))
+        cap = int(want[1].size) + 8
+        bats.append(dict(n=n, want=want, cap=cap, data=torch.from_numpy(data.copy()).to(dev),
+                         off=torch.from_numpy(offsets.view(np.int64).copy()).to(dev),
+                         loff=[torch.zeros(n + 1, dtype=torch.int64, device=dev) for _ in range(2)],
+                         locs=[torch.zeros(cap, dtype=torch.int32, device=dev) for _ in range(2)],
+                         need=torch.zeros(1, dtype=torch.int64, device=dev)))
+    ws = ix.locate_workspace_size(max(sizes))
+    d_ws = torch.zeros(ws, dtype=torch.uint8, device=dev)
+    jobs = []
+    for i in range(200):
+        b = bats[i % len(bats)]
+        k = (i // len(bats)) % 2  # alternate output buffers: launch i's outputs survive launch i + 4
+        jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), b["n"], b["loff"][k].data_ptr(),
+                                  b["locs"][k].data_ptr(), b["cap"], b["need"].data_ptr(), d_ws.data_ptr(), ws))
+    q = ix.job_queue(jobs)
+    for rep in range(2):
+        ix.locate_jobs_async(q)
+        ix.sync()
+        for b in bats:
+            for k in range(2):
+                assert np.array_equal(b["loff"][k].cpu().numpy().view(np.uint64), b["want"][0])
+                got = b["locs"][k].cpu().numpy()[:b["want"][1].size].view(np.uint32)
+                assert np.array_equal(got, b["want"][1])
+            assert int(b["need"].item()) == b["want"][1].size
+    ix.close()
