@@ -96,8 +96,8 @@ def phase_stamps(pkg, ix, step, B, out_path):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--text-len", type=int, default=0, help="override the config's text length")
     ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU per step (weak scaling)")
@@ -120,7 +120,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight: step i runs batch i %% S on HIP stream i %% S (each stream its own "
                          "patterns, outputs and look-back workspace), as a serving loop pipelines batches")
     ap.add_argument("--batches", type=int, default=8,
@@ -235,21 +235,23 @@ def main():
 
     d_cnt = torch.zeros(B, dtype=pdt_t, device=dev)
 
+    stage_kb = min(56, -(-256 * m // 1024))  # FMX_HINT_STAGE_KB: every tile spans 256 * m bytes
+
     def job(bt):
         return ix.locate_job(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, bt["loff"].data_ptr(),
                              bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
-                             stream=bt["stream"].cuda_stream, long_patterns=m > 64)
+                             stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
 
     def step():
         bt = batches[state["i"] % NB]
         state["i"] += 1
         if args.count_only:  # diagnostic: the search alone (k_count)
             ix.count_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, d_cnt.data_ptr(),
-                                 stream=bt["stream"].cuda_stream, long_patterns=m > 64)
+                                 stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
             return
         ix.locate_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, bt["loff"].data_ptr(),
                               bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
-                              stream=bt["stream"].cuda_stream, long_patterns=m > 64)
+                              stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
 
     # native submission: the K steps of the timed region as one queue of K
     # jobs (step i = batch i % NB), issued by one fmx_locate_jobs_async call

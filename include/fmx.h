@@ -62,7 +62,12 @@ typedef struct fmx_layout {
                                    (src/locate/with_rev_iter.rs:5-38)                          */
 #define FMX_HINT_LONG_PATTERNS 2u /* performance hint: patterns average more than 64 bytes; the
                                    kernels stage each workgroup's patterns in 56 KB of LDS
-                                   instead of 16 KB (set automatically by the host-buffer calls) */
+                                   instead of 16 KB                                            */
+/* Performance hint: stage each 256-pattern tile in kb KB of LDS (1..56): the
+ * most bytes any tile's patterns span.  A tile that does not fit is read from
+ * HBM instead (same results).  Less LDS per workgroup = more workgroups per
+ * CU.  Overrides FMX_HINT_LONG_PATTERNS; the host-buffer calls set it exactly. */
+#define FMX_HINT_STAGE_KB(kb) ((((uint32_t)(kb)) & 0xffu) << 8)
 
 /* Load options: device-side structures derived from the blob at load time.
  * Results are identical with any combination; they trade HBM for fewer

@@ -324,6 +324,13 @@ def _options(occ: str, deep_lut: bool, full_sa: bool = True, text: bool = True, 
             | (_n.FMX_OPT_LUT_ROWS if lut_rows else 0))
 
 
+def _flags(reversed: bool, long_patterns: bool, stage_kb: int = 0) -> int:
+    """Query flags: FMX_PATTERN_REVERSED, FMX_HINT_LONG_PATTERNS, and
+    FMX_HINT_STAGE_KB(stage_kb) (LDS KB per 256-pattern tile; 0 = no hint)."""
+    return ((_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
+            | ((int(stage_kb) & 0xFF) << 8))
+
+
 def _ptr(a: Optional[np.ndarray]):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
@@ -525,8 +532,8 @@ class FmIndex:
 
     # -- device-resident API (pointers are ints; stream is a hipStream_t) --
     def count_batch_async(self, d_bytes: int, d_offsets: int, n: int, d_counts: int,
-                          stream: int = 0, reversed: bool = False, long_patterns: bool = False) -> None:
-        flags = (_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
+                          stream: int = 0, reversed: bool = False, long_patterns: bool = False, stage_kb: int = 0) -> None:
+        flags = _flags(reversed, long_patterns, stage_kb)
         _check(_n.lib().fmx_count_batch_async(self._h, C.c_void_p(d_bytes), C.c_void_p(d_offsets), n, flags,
                                               C.c_void_p(d_counts), C.c_void_p(stream) if stream else None))
 
@@ -538,9 +545,9 @@ class FmIndex:
     def locate_batch_async(self, d_bytes: int, d_offsets: int, n: int, d_loc_offsets: int,
                            d_locs: int, cap: int, d_needed: int, d_ws: int, ws_bytes: int,
                            d_counts: int = 0, stream: int = 0, reversed: bool = False,
-                           long_patterns: bool = False) -> None:
+                           long_patterns: bool = False, stage_kb: int = 0) -> None:
         """`long_patterns`: FMX_HINT_LONG_PATTERNS (patterns average > 64 bytes)."""
-        flags = (_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
+        flags = _flags(reversed, long_patterns, stage_kb)
         _check(_n.lib().fmx_locate_batch_async(
             self._h, C.c_void_p(d_bytes), C.c_void_p(d_offsets), n, flags,
             C.c_void_p(d_counts) if d_counts else None, C.c_void_p(d_loc_offsets), C.c_void_p(d_locs), cap,
@@ -550,10 +557,10 @@ class FmIndex:
     @staticmethod
     def locate_job(d_bytes: int, d_offsets: int, n: int, d_loc_offsets: int, d_locs: int, cap: int,
                    d_needed: int, d_ws: int, ws_bytes: int, d_counts: int = 0, stream: int = 0,
-                   reversed: bool = False, long_patterns: bool = False) -> "_n.fmx_locate_job":
+                   reversed: bool = False, long_patterns: bool = False, stage_kb: int = 0) -> "_n.fmx_locate_job":
         """One entry of a locate queue (fmx_locate_job): the arguments of
         locate_batch_async."""
-        flags = (_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
+        flags = _flags(reversed, long_patterns, stage_kb)
         return _n.fmx_locate_job(d_bytes, d_offsets, n, flags, 0, d_counts or None, d_loc_offsets, d_locs, cap,
                                  d_needed, d_ws, ws_bytes, stream or None)
 

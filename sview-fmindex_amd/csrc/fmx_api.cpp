@@ -653,6 +653,15 @@ static fmx_status check_patterns(const uint64_t *offsets, uint64_t n) {
     return FMX_OK;
 }
 
+// FMX_HINT_STAGE_KB for a host batch: the most bytes any 256-pattern tile
+// spans, rounded up to whole KB (tiles past 56 KB read their patterns from HBM).
+static uint32_t stage_hint(const uint64_t *offsets, uint64_t n) {
+    uint64_t most = 0;
+    for (uint64_t t = 0; t < n; t += 256) most = std::max(most, offsets[std::min(n, t + 256)] - offsets[t]);
+    const uint64_t kb = std::min<uint64_t>(std::max<uint64_t>((most + 1023) / 1024, 1), kStageBytesLong / 1024);
+    return FMX_HINT_STAGE_KB(kb);
+}
+
 fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets, uint64_t n,
                            uint32_t flags, void *out_counts) {
     if (!ix || (n && (!offsets || !out_counts))) return FMX_E_ARG;
@@ -670,7 +679,7 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return FMX_E_DEVICE;
-    if (nb > 64 * n) flags |= FMX_HINT_LONG_PATTERNS;
+    flags |= stage_hint(offsets, n);
     st = fmx_count_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, d + o_cnt, s);
     if (st) return st;
     if (hipMemcpyAsync(out_counts, d + o_cnt, n * pb, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
@@ -706,7 +715,7 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
     if (st) return st;
     hipSetDevice(ix->device);
     const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
-    if (nb > 64 * n) flags |= FMX_HINT_LONG_PATTERNS;
+    flags |= stage_hint(offsets, n);
     st = ensure_ws(ix, n);
     if (st) return st;
     const uint64_t o_off = align_up(nb, 256);

@@ -202,36 +202,55 @@ struct PatView {
     FMX_HD uint32_t at(uint64_t j) const { return sym ? sym[j] : enc[raw[rev ? m - 1 - j : j]]; }
 };
 
-// Four text symbols t[a..a+4) from two aligned words (the text buffer is
-// padded by 16 bytes past n).
-FMX_HD uint32_t load4(const uint8_t *t, uint64_t a) {
-    const uint64_t al = a & ~3ull;
-    const uint32_t sh = (uint32_t)(a & 3) * 8;
-    const uint32_t w0 = *reinterpret_cast<const uint32_t *>(t + al);
-    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(t + al + 4);
-    return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
-}
-
 // Single-row tail (FMX_OPT_TEXT): the interval of P[idx..m) is the one row
 // whose suffix starts at text position x, so P occurs at most once, at
 // x - idx.  The LF loop would consume P[idx-1], P[idx-2], ... and stop at the
 // first symbol that does not precede the suffix (or at the text start); here
-// the same positions are compared with T[x-1], T[x-2], ... four at a time.
-// Only positions below `top` are compared (top = idx: all of them).
-// Returns the highest position jm that fails (-1: P occurs at x - idx).
-template <typename P>
-FMX_HD int64_t tail_mismatch(const QueryArgs &a, const PatView &pv, uint64_t idx, uint64_t x, uint64_t top) {
+// the same positions are compared with T[x-1], T[x-2], ..., 64 per round: the
+// round's text bytes are five aligned 16-B vectors, all in flight at once
+// (the text buffer is padded by 16 bytes past n), compared word by word
+// against the staged pattern symbols.  Only positions below `top` are
+// compared (top = idx: all of them).  Returns the highest position jm that
+// fails (-1: P occurs at x - idx).
+// One out-of-line copy (not one per kernel instantiation): it only touches
+// the text and the pattern.
+__host__ __device__ __noinline__ inline int64_t tail_mismatch(const uint8_t *text, PatView pv, uint64_t idx,
+                                                              uint64_t x, uint64_t top) {
+    using V4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint64_t lowest = idx > x ? idx - x : 0;  // positions below have no text before them
     const uint64_t tb = x - idx;                     // text position of P[0] (mod 2^64)
     uint64_t hj = top;
     while (hj > lowest) {
-        const uint64_t lj = hj - lowest >= 4 ? hj - 4 : lowest;
-        const uint32_t tw = load4(a.text, tb + lj);
-        uint32_t mism = 0;
+        const uint64_t lj = hj - lowest > 64 ? hj - 64 : lowest;
+        const uint64_t t0 = tb + lj, t1 = tb + hj;  // text range [t0, t1), at most 64 bytes
+        const uint64_t a0 = t0 & ~15ull;
+        const V4 *src = reinterpret_cast<const V4 *>(text + a0);
+        V4 v[5];
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u)
-            if (lj + u < hj && ((tw >> (8 * u)) & 0xffu) != pv.at(lj + u)) mism |= 1u << u;
-        if (mism) return (int64_t)(lj + (31 - __builtin_clz(mism)));
+        for (uint32_t u = 0; u < 5; ++u) {
+            if (a0 + 16ull * u < t1) v[u] = src[u];
+            else v[u] = V4{0u, 0u, 0u, 0u};
+        }
+        int64_t best = -1;  // positions rise with (u, w): the last mismatching word holds the highest
+#pragma unroll
+        for (uint32_t u = 0; u < 5; ++u) {
+#pragma unroll
+            for (uint32_t w = 0; w < 4; ++w) {
+                const uint64_t base = a0 + 16ull * u + 4ull * w;
+                if (base + 4 <= t0 || base >= t1) continue;
+                uint32_t pw = 0, valid = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint64_t tp = base + b;
+                    const bool in = tp >= t0 && tp < t1;
+                    pw |= (in ? pv.at(tp - tb) : 0u) << (8 * b);
+                    valid |= in ? 0xffu << (8 * b) : 0u;
+                }
+                const uint32_t d = (v[u][w] ^ pw) & valid;
+                if (d) best = (int64_t)(base + (uint64_t)((31 - __builtin_clz(d)) >> 3) - tb);
+            }
+        }
+        if (best >= 0) return best;
         hj = lj;
     }
     return lowest > 0 ? (int64_t)(lowest - 1) : -1;
@@ -275,7 +294,10 @@ FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo
     for (uint64_t vb = v0; vb < v1; vb += NV) {
         V4 x[NV];
 #pragma unroll
-        for (uint32_t u = 0; u < NV; ++u) x[u] = vec[vb + u < v1 ? vb + u : v1 - 1];
+        for (uint32_t u = 0; u < NV; ++u) {
+            if (vb + u < v1) x[u] = vec[vb + u];  // (no duplicate requests past the interval)
+            else x[u] = V4{0u, 0u, 0u, 0u};
+        }
 #pragma unroll
         for (uint32_t u = 0; u < NV; ++u) {
 #pragma unroll
@@ -303,7 +325,7 @@ FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo
         for (uint64_t m2 = msk; m2; m2 &= m2 - 1) {
             const uint64_t b = (uint64_t)__builtin_ctzll(m2);
             const P x = sa[2 * ((uint64_t)lo + b)];
-            if (tail_mismatch<P>(a, pv, idx, (uint64_t)x, idx - Cl) < 0) {
+            if (tail_mismatch(a.text, pv, idx, (uint64_t)x, idx - Cl) < 0) {
                 if (!keep) first = x;
                 keep |= 1ull << b;
             }
@@ -353,7 +375,7 @@ FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w
     const uint64_t diff = (pc ^ (uint64_t)(w0 & (P)~row_flag<P>())) & keep;
     int64_t jm;
     if (diff) jm = (int64_t)(idx - 1 - (uint64_t)__builtin_ctzll(diff) / bps);
-    else jm = idx > Ld ? tail_mismatch<P>(a, pv, idx, x, idx - Ld) : -1;
+    else jm = idx > Ld ? tail_mismatch(a.text, pv, idx, x, idx - Ld) : -1;
     mode = kHitOne;
     lo = 0;
     hi = 0;
@@ -438,7 +460,7 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
         }
         if (a.text != nullptr && hi - lo == P(1)) {
             const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[(uint64_t)lo * a.sa_stride];
-            const int64_t jm = tail_mismatch<P>(a, pv, idx, x, idx);
+            const int64_t jm = tail_mismatch(a.text, pv, idx, x, idx);
             mode = kHitOne;
             if (jm >= 0) {
                 // the LF loop reads (and would reject) the symbol at jm before

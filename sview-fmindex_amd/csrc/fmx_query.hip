@@ -657,6 +657,8 @@ static inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads +
 uint64_t locate_tiles_cap(uint64_t n) { return (n + 255) / 256 > 0 ? (n + 255) / 256 : 1; }
 
 static inline uint32_t stage_bytes_for(uint32_t flags) {
+    const uint32_t kb = (flags >> 8) & 0xffu;  // FMX_HINT_STAGE_KB
+    if (kb) return std::min<uint32_t>(kb, kStageBytesLong / 1024) * 1024u;
     return (flags & FMX_HINT_LONG_PATTERNS) ? (uint32_t)kStageBytesLong : (uint32_t)kStageBytes;
 }
 

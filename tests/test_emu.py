@@ -152,3 +152,27 @@ def test_device_code_absent_symbols(emu, O):
                 st, cnt, locs = emu_locate(emu, blob, layout, options, [p])
                 got = ("ok", [int(x) for x in locs]) if st == 0 else ("err", st)
                 assert got == want, (p, options, got, want)
+
+
+def test_device_code_long_tails(emu, O):
+    """Long patterns (C5-like, up to 200 symbols): single-row tails compared
+    against the text 64 positions per round, with one substituted symbol at
+    every depth of the tail, and tails that run past the text start."""
+    rng = np.random.default_rng(5150)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000))
+    alt = {ord("A"): b"C", ord("C"): b"G", ord("G"): b"T", ord("T"): b"A"}
+    pats = []
+    for s in rng.integers(0, 19700, size=60):
+        m = int(rng.integers(40, 201))
+        p = text[s:s + m]
+        pats.append(p)
+        j = int(rng.integers(0, len(p)))
+        pats.append(p[:j] + alt[p[j]] + p[j + 1:])
+    for m in (63, 64, 65, 129, 150):  # the text start falls inside the tail
+        pats.append(b"G" * (m - 50) + text[:50])
+        pats.append(text[:m])
+    for layout in [(4, 3, 64, 0), (8, 3, 128, 0)]:
+        blob = O.build(text, 5, O.layout(*layout[:3]), 3, 2, table)
+        for options in OPTIONS:
+            check(emu, O, blob, layout, pats, options)
