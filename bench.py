@@ -120,11 +120,14 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--streams", type=int, default=8,
-                    help="batches in flight: step i runs batch i %% S on HIP stream i %% S (each stream its own "
-                         "patterns, outputs and look-back workspace), as a serving loop pipelines batches")
-    ap.add_argument("--batches", type=int, default=8,
+    ap.add_argument("--streams", type=int, default=2,
+                    help="launches in flight: launch q runs on HIP stream q %% S (each stream its own batches: "
+                         "patterns, outputs and look-back workspaces), as a serving loop pipelines batches")
+    ap.add_argument("--batches", type=int, default=16,
                     help="distinct pattern batches cycled over the steps (at least --streams)")
+    ap.add_argument("--group", type=int, default=4,
+                    help="batches per kernel launch in the timed region (fmx_locate_group_async, at most 8; "
+                         "1 = one launch per batch)")
     ap.add_argument("--submit", default="native", choices=["native", "python"],
                     help="native: the timed steps are issued as one fmx_locate_jobs_async queue; "
                          "python: one fmx_locate_batch_async call per step")
@@ -206,11 +209,15 @@ def main():
 
     # ---- patterns: substrings at uniform starts (per-rank, per-batch seed) ---
     # NB distinct batches (each its own patterns, outputs and look-back
-    # workspace), batch b always on stream b % S; step i runs batch i % NB, so
-    # consecutive passes over one batch are NB steps apart (their index lines
-    # are not still cached).  Batch 0 is the one checked against the CPU oracle.
+    # workspace).  Steps run in groups of GR batches per kernel launch
+    # (fmx_locate_group_async), group q on stream q % S using batches
+    # [(q % S) * GR, (q % S) * GR + GR): a batch always runs on the same
+    # stream, and consecutive passes over one batch are S * GR steps apart
+    # (their index lines are not still cached).  Batch 0 is the one checked
+    # against the CPU oracle.
     S = max(1, args.streams)
-    NB = max(S, args.batches)
+    GR = max(1, min(args.group, 8))
+    NB = max(S * GR, args.batches)
     cap = 4 * B + 4096
     ws = ix.locate_workspace_size(B)
     streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
@@ -220,7 +227,7 @@ def main():
         pg.manual_seed(args.seed * 1000 + 7 + rank + 100003 * bi)
         starts = torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg)
         batches.append(dict(
-            stream=streams[bi % S],
+            stream=streams[(bi // GR) % S],
             starts=starts,
             pat=d_text[(starts[:, None] + torch.arange(m, device=dev)[None, :]).reshape(-1)].contiguous(),
             off=(torch.arange(B + 1, device=dev, dtype=torch.int64) * m).contiguous(),
@@ -253,10 +260,16 @@ def main():
                               bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
                               stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
 
-    # native submission: the K steps of the timed region as one queue of K
-    # jobs (step i = batch i % NB), issued by one fmx_locate_jobs_async call
+    # native submission: the K steps of the timed region as ceil(K / GR)
+    # grouped launches (GR = 1: one queue of K single-batch jobs)
     native = args.submit == "native" and not args.count_only
-    queue = ix.job_queue([job(batches[i % NB]) for i in range(args.steps)]) if native else None
+    queue, groups = None, []
+    if native and GR == 1:
+        queue = ix.job_queue([job(batches[i % NB]) for i in range(args.steps)])
+    elif native:
+        for q, i0 in enumerate(range(0, args.steps, GR)):
+            sel = [batches[((q % S) * GR + t) % NB] for t in range(min(GR, args.steps - i0))]
+            groups.append((ix.job_queue([job(bt) for bt in sel]), sel[0]["stream"].cuda_stream))
 
     for _ in range(max(args.warmup, NB)):
         step()
@@ -275,8 +288,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    if native:
+    if native and GR == 1:
         ix.locate_jobs_async(queue)
+    elif native:
+        for gq, gs in groups:
+            ix.locate_group_async(gq, stream=gs)
     else:
         for _ in range(args.steps):
             step()
@@ -325,10 +341,14 @@ def main():
     if args.count_only:
         dominant = "count"
         kern.pop("locate", None)
-    alg_bytes = per_pattern * B + per_occ * total_occ
+    # a launch covers GR batches when grouped: patterns per timed launch
+    # from the engine's own counters
+    t_dom = timing.get(dominant, {})
+    pats_per_launch = t_dom["units"] / t_dom["launches"] if t_dom.get("launches") else B
+    alg_bytes = (per_pattern + per_occ * total_occ / B) * pats_per_launch
     achieved = alg_bytes / (kern[dominant] * 1e-3) / 1e9
     traffic, traffic_src = None, None
-    key = f"{args.config}:{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}"
+    key = f"{args.config}:{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}" + (f":g{GR}" if native and GR > 1 else "")
     if os.path.exists(args.traffic_json):
         try:
             pm = json.load(open(args.traffic_json))
@@ -381,17 +401,18 @@ def main():
             "load_options": info["options"], "deep_lut_k": info["deep_lut_k"],
             "index_hbm_bytes": info["device_bytes"],
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
-            "streams": S, "distinct_batches": NB, "submit": "native" if native else "python",
+            "streams": S, "batches_per_launch": GR if native else 1, "distinct_batches": NB, "submit": "native" if native else "python",
         },
         "roofline": {
             "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-            "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pattern": alg_bytes / B,
+            "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pattern": alg_bytes / pats_per_launch,
+            "patterns_per_launch": pats_per_launch,
             "avg_launch_ms": kern.get(dominant),
             # the binding resource of a dependent-gather kernel: 64-B HBM line
             # requests per second vs the measured random-line ceiling
             # (scripts/micro/randline.hip, profiles/r01_randline.jsonl)
-            "hbm_lines_per_pattern": None if traffic is None else traffic / 64 / B,
+            "hbm_lines_per_pattern": None if traffic is None else traffic / 64 / pats_per_launch,
             "hbm_glines_per_s": None if traffic is None else traffic / 64 / (kern[dominant] * 1e-3) / 1e9,
             "random_line_ceiling_glines_per_s": RANDOM_LINE_CEILING,
         },

@@ -574,6 +574,11 @@ class FmIndex:
         (fmx_locate_jobs_async): no per-batch Python overhead."""
         _check(_n.lib().fmx_locate_jobs_async(self._h, queue, len(queue)))
 
+    def locate_group_async(self, queue, stream: int = 0) -> None:
+        """Run a queue of locate batches together, up to 8 per kernel launch,
+        on `stream` (fmx_locate_group_async); distinct workspaces and outputs."""
+        _check(_n.lib().fmx_locate_group_async(self._h, queue, len(queue), C.c_void_p(stream) if stream else None))
+
     def sync(self, stream: int = 0) -> None:
         _check(_n.lib().fmx_sync(self._h, C.c_void_p(stream) if stream else None))
 

@@ -86,6 +86,7 @@ SIGNATURES = {
     "fmx_locate_workspace_size": (_i, [_p, _u64, _PU64]),
     "fmx_locate_batch_async": (_i, [_p, _p, _p, _u64, _u32, _p, _p, _p, _u64, _p, _p, _u64, _p]),
     "fmx_locate_jobs_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64]),
+    "fmx_locate_group_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64, _p]),
     "fmx_sync": (_i, [_p, _p]),
     "fmx_timing_enable": (_i, [_p, _i]),
     "fmx_timing_read": (_i, [_p, C.POINTER(fmx_kernel_timing), _i, C.POINTER(_i)]),

@@ -587,6 +587,26 @@ fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes)
     return FMX_OK;
 }
 
+// The next look-back epoch of a workspace (k_locate); after kLocateEpochs
+// launches, the tiles any of them published are zeroed (stream-ordered before
+// this launch) and the epochs start again.
+static fmx_status next_epoch(fmx_index *ix, void *d_ws, uint64_t tiles, hipStream_t s, uint32_t *epoch) {
+    uint64_t clear_tiles = 0;
+    {
+        std::lock_guard<std::mutex> g(ix->ws_mu);
+        fmx_index::WsState &w = ix->ws_state[d_ws];
+        if (w.epoch >= kLocateEpochs) {
+            clear_tiles = w.hi_tiles;
+            w.epoch = 0;
+        }
+        *epoch = ++w.epoch;
+        w.hi_tiles = std::max(w.hi_tiles, tiles);
+    }
+    if (clear_tiles && hipMemsetAsync((uint8_t *)d_ws + 256, 0, clear_tiles * 8, s) != hipSuccess)
+        return FMX_E_DEVICE;
+    return FMX_OK;
+}
+
 fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                   uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs,
                                   uint64_t cap, uint64_t *d_needed, void *d_ws, uint64_t ws_bytes, void *stream) {
@@ -602,23 +622,7 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
     uint8_t *ws = (uint8_t *)d_ws;
     const uint64_t G = locate_tiles_cap(n);
     uint32_t epoch = 0;
-    if (ix->locate_fused) {
-        // The next look-back epoch of this workspace; after kLocateEpochs
-        // launches, the tiles any of them published are zeroed (stream-ordered
-        // before this launch) and the epochs start again.
-        uint64_t clear_tiles = 0;
-        {
-            std::lock_guard<std::mutex> g(ix->ws_mu);
-            fmx_index::WsState &w = ix->ws_state[d_ws];
-            if (w.epoch >= kLocateEpochs) {
-                clear_tiles = w.hi_tiles;
-                w.epoch = 0;
-            }
-            epoch = ++w.epoch;
-            w.hi_tiles = std::max(w.hi_tiles, G);
-        }
-        if (clear_tiles && hipMemsetAsync(ws + 256, 0, clear_tiles * 8, s) != hipSuccess) return FMX_E_DEVICE;
-    }
+    if (ix->locate_fused && next_epoch(ix, d_ws, G, s, &epoch) != FMX_OK) return FMX_E_DEVICE;
     return dev_err(timed(ix, "locate", s, n, [&] {
         return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
                              (uint32_t *)ws, (uint64_t *)(ws + 256), G, epoch, s);
@@ -632,6 +636,67 @@ fmx_status fmx_locate_jobs_async(fmx_index *ix, const fmx_locate_job *jobs, uint
         const fmx_status st =
             fmx_locate_batch_async(ix, j.d_bytes, j.d_offsets, j.n_patterns, j.flags, j.d_counts, j.d_loc_offsets,
                                    j.d_locs, j.cap, j.d_needed, j.d_workspace, j.workspace_bytes, j.stream);
+        if (st) return st;
+    }
+    return FMX_OK;
+}
+
+fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs, void *stream) {
+    if (!ix || (n_jobs && !jobs)) return FMX_E_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    for (uint64_t i = 0; i < n_jobs; ++i) {
+        const fmx_locate_job &j = jobs[i];
+        if (!j.d_loc_offsets || !j.d_needed || (j.n_patterns && (!j.d_bytes || !j.d_offsets)) ||
+            (j.cap && !j.d_locs) || !j.d_workspace || j.workspace_bytes < ws_bytes_for(ix, j.n_patterns) ||
+            j.reserved != 0)
+            return FMX_E_ARG;
+        for (uint64_t k = 0; k < i; ++k)
+            if (jobs[k].d_workspace == j.d_workspace) return FMX_E_ARG;  // one look-back per workspace
+    }
+    if (!ix->locate_fused) {  // the split kernels: one batch after another
+        for (uint64_t i = 0; i < n_jobs; ++i) {
+            const fmx_locate_job &j = jobs[i];
+            const fmx_status st =
+                fmx_locate_batch_async(ix, j.d_bytes, j.d_offsets, j.n_patterns, j.flags, j.d_counts,
+                                       j.d_loc_offsets, j.d_locs, j.cap, j.d_needed, j.d_workspace,
+                                       j.workspace_bytes, s);
+            if (st) return st;
+        }
+        return FMX_OK;
+    }
+    // up to kMaxGroup non-empty batches per launch; empty ones get their
+    // zero offset and total directly
+    uint64_t i = 0;
+    while (i < n_jobs) {
+        LocateGroup grp{};
+        uint32_t stage = 0, tiles = 0;
+        uint64_t units = 0;
+        for (; i < n_jobs && grp.n < kMaxGroup; ++i) {
+            const fmx_locate_job &j = jobs[i];
+            if (j.n_patterns == 0) {
+                hipError_t e = hipMemsetAsync(j.d_loc_offsets, 0, 8, s);
+                if (e == hipSuccess) e = hipMemsetAsync(j.d_needed, 0, 8, s);
+                if (e != hipSuccess) return FMX_E_DEVICE;
+                continue;
+            }
+            const uint64_t G = locate_tiles_cap(j.n_patterns);
+            uint32_t epoch = 0;
+            if (next_epoch(ix, j.d_workspace, G, s, &epoch) != FMX_OK) return FMX_E_DEVICE;
+            grp.tile_begin[grp.n] = tiles;
+            grp.b[grp.n++] = LocateBatch{j.d_bytes, j.d_offsets, j.n_patterns, j.d_counts, j.d_loc_offsets,
+                                         j.d_locs, j.cap, j.d_needed, (uint64_t *)((uint8_t *)j.d_workspace + 256),
+                                         epoch, (j.flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
+            tiles += (uint32_t)G;
+            units += j.n_patterns;
+            // the launch stages with the largest hint of its batches
+            const uint32_t kb = (j.flags >> 8) & 0xffu, kbs = (stage >> 8) & 0xffu;
+            if (kb > kbs) stage = (stage & ~0xff00u) | (kb << 8);
+            stage |= j.flags & FMX_HINT_LONG_PATTERNS;
+        }
+        if (grp.n == 0) continue;
+        const fmx_status st = dev_err(timed(ix, "locate", s, units, [&] {
+            return launch_locate_group(ix, grp, stage, s);
+        }));
         if (st) return st;
     }
     return FMX_OK;

@@ -161,6 +161,29 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                          uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
                          uint32_t epoch, hipStream_t stream);
 constexpr uint32_t kLocateEpochs = 63;  // k_locate tile words carry 6 bits of epoch
+// One batch of a k_locate launch; a launch runs up to kMaxGroup of them, each
+// with its own patterns, outputs and look-back tiles (fmx_locate_group_async).
+constexpr uint32_t kMaxGroup = 8;
+struct LocateBatch {
+    const uint8_t *bytes;
+    const uint64_t *offs;
+    uint64_t npat;
+    void *out_cnt;  // optional P-wide counts
+    uint64_t *loc_off;
+    void *out_locs;
+    uint64_t cap;
+    uint64_t *needed;
+    uint64_t *tiles;
+    uint32_t epoch;
+    uint32_t rev;
+};
+struct LocateGroup {
+    LocateBatch b[kMaxGroup];
+    uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
+    uint32_t n;
+};
+hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
+                               hipStream_t stream);
 uint64_t locate_tiles_cap(uint64_t n);
 // Bytes per pattern of the search-result records in the locate workspace.
 uint64_t locate_rec_bytes(uint32_t pos_bytes);

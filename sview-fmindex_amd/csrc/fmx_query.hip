@@ -224,30 +224,41 @@ __device__ __forceinline__ void emit_locations(const QueryArgs &a, const P *C, u
 constexpr uint64_t kTileAgg = 1, kTileInc = 2;
 
 template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const uint8_t *__restrict__ bytes,
-                                                const uint64_t *__restrict__ offs, uint64_t npat, uint32_t flags,
-                                                P *__restrict__ out_cnt, uint64_t *__restrict__ loc_off,
-                                                P *__restrict__ out_locs, uint64_t cap, uint64_t *__restrict__ needed,
-                                                uint64_t *__restrict__ tiles, uint32_t epoch,
-                                                uint32_t stage_bytes) {
+__global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const LocateGroup grp, uint32_t stage_bytes) {
     __shared__ Tables<P> s;
     extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     __shared__ uint64_t s_scan[4];
     __shared__ uint64_t s_prefix;
     FMX_STAMP(0, __builtin_amdgcn_s_memrealtime());
     stage_tables(a, s);
+    // This workgroup's batch (workgroup-uniform: scalar kernel-argument reads).
+    uint32_t jb = 0;
+#pragma unroll
+    for (uint32_t t = 1; t < kMaxGroup; ++t)
+        if (t < grp.n && blockIdx.x >= grp.tile_begin[t]) jb = t;
+    const LocateBatch &B = grp.b[jb];
+    const uint8_t *__restrict__ bytes = B.bytes;
+    const uint64_t *__restrict__ offs = B.offs;
+    const uint64_t npat = B.npat;
+    P *__restrict__ out_cnt = (P *)B.out_cnt;
+    uint64_t *__restrict__ loc_off = B.loc_off;
+    P *__restrict__ out_locs = (P *)B.out_locs;
+    const uint64_t cap = B.cap;
+    uint64_t *__restrict__ needed = B.needed;
+    uint64_t *__restrict__ tiles = B.tiles;
+    const uint32_t epoch = B.epoch;
     const uint32_t G = (uint32_t)((npat + 255) / 256);
-    // Tile g = blockIdx.x.  The look-back below waits only on lower tiles, and
-    // workgroups are dispatched in increasing id order (per XCD, round-robin
-    // over XCDs), so every tile waited on is running or done.  (A ticket
-    // taken with one device-scope atomic per workgroup would guarantee the
-    // same at the price of 391 serialised atomics on one address before any
-    // pattern is read — 5-10 us of a 30 us launch, measured.)
-    const uint32_t g = blockIdx.x;
+    // Tile g of the batch.  The look-back below waits only on lower tiles of
+    // the same batch, and workgroups are dispatched in increasing id order
+    // (per XCD, round-robin over XCDs), so every tile waited on is running or
+    // done.  (A ticket taken with one device-scope atomic per workgroup would
+    // guarantee the same at the price of serialised atomics on one address
+    // before any pattern is read — 5-10 us of a 30 us launch, measured.)
+    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
     FMX_STAMP(6, __builtin_amdgcn_s_memrealtime());
 
     // ---- 1. SA interval of every pattern of the tile ----------------------
-    const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
+    const bool rev = B.rev != 0;
     uint64_t beg, end, b0, b1;
     const bool staged =
         stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end, b0, b1);
@@ -683,9 +694,11 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         const uint32_t sb = stage_bytes_for(flags);
         if (ix->locate_fused) {
-            hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
-                               d_offsets, n, flags, (P *)d_counts, d_loc_offsets, (P *)d_locs, cap, d_needed,
-                               d_tiles, epoch, sb);
+            LocateGroup grp{};
+            grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles,
+                                   epoch, (flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
+            grp.n = 1;
+            hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, grp, sb);
             return hipGetLastError();
         }
         // workspace: [tile counts: tiles_cap][tile offsets: tiles_cap][records: n]
@@ -696,6 +709,23 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                            d_needed, sb);
         hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, n,
                            (const SearchRec<P> *)recs, (const uint64_t *)tile_off, d_loc_offsets, (P *)d_locs, cap);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
+                               hipStream_t stream) {
+    if (grp.n == 0 || grp.n > kMaxGroup || grp.tile_begin[0] != 0) return hipErrorInvalidValue;
+    uint64_t tiles = 0;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        if (grp.b[j].npat == 0 || grp.tile_begin[j] != tiles) return hipErrorInvalidValue;
+        if (grp.b[j].epoch == 0 || grp.b[j].epoch > kLocateEpochs) return hipErrorInvalidValue;
+        tiles += (grp.b[j].npat + 255) / 256;
+    }
+    if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
+        const uint32_t sb = stage_bytes_for(stage_flags);
+        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa, grp, sb);
         return hipGetLastError();
     });
 }

@@ -430,3 +430,54 @@ def test_locate_queue_many_launches_one_workspace(pkg, O):
                 assert np.array_equal(got, b["want"][1])
             assert int(b["need"].item()) == b["want"][1].size
     ix.close()
+
+
+def test_locate_group_launch(pkg, O):
+    """fmx_locate_group_async: up to 8 batches per k_locate launch (more are
+    split over launches), sizes from 0 to a few thousand, forward and
+    reversed, each batch's outputs equal to the host API's; repeated so the
+    workspaces' look-back epochs wrap; a shared workspace is rejected."""
+    import torch
+    rng = np.random.default_rng(33)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=120_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    dev = torch.device("cuda:0")
+    sizes = [2500, 0, 1, 700, 256, 257, 3000, 40, 1999, 5, 1024]  # 11 batches: two launches
+    bats, jobs = [], []
+    for bi, n in enumerate(sizes):
+        rev = bi % 3 == 2
+        starts = rng.integers(0, text.size - 30, size=n)
+        pats = [text[s:s + int(rng.integers(1, 31))].tobytes() for s in starts]
+        want = ix.locate_batch(pats)
+        q = [p[::-1] for p in pats] if rev else pats
+        data, offsets = pkg.pack_patterns(q)
+        cap = int(want[1].size) + 8
+        b = dict(n=n, want=want, data=torch.from_numpy(np.concatenate([data, np.zeros(1, np.uint8)])).to(dev),
+                 off=torch.from_numpy(offsets.view(np.int64).copy()).to(dev),
+                 loff=torch.full((n + 1,), -1, dtype=torch.int64, device=dev),
+                 locs=torch.zeros(cap, dtype=torch.int32, device=dev), need=torch.zeros(1, dtype=torch.int64, device=dev),
+                 cnt=torch.zeros(max(n, 1), dtype=torch.int32, device=dev))
+        ws = ix.locate_workspace_size(max(n, 1))
+        b["ws"] = torch.zeros(ws, dtype=torch.uint8, device=dev)
+        jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), n, b["loff"].data_ptr(),
+                                  b["locs"].data_ptr(), cap, b["need"].data_ptr(), b["ws"].data_ptr(), ws,
+                                  d_counts=b["cnt"].data_ptr(), reversed=rev, stage_kb=2 + bi % 3))
+        bats.append(b)
+    q = ix.job_queue(jobs)
+    stream = torch.cuda.Stream(device=dev)
+    for rep in range(70):
+        ix.locate_group_async(q, stream=stream.cuda_stream)
+    ix.sync(stream.cuda_stream)
+    for b in bats:
+        wo, wl = b["want"]
+        assert np.array_equal(b["loff"].cpu().numpy().view(np.uint64), wo)
+        assert np.array_equal(b["locs"].cpu().numpy()[:wl.size].view(np.uint32), wl)
+        assert int(b["need"].item()) == wl.size
+        if b["n"]:
+            assert np.array_equal(b["cnt"].cpu().numpy()[:b["n"]].view(np.uint32), np.diff(wo).astype(np.uint32))
+    dup = ix.job_queue([jobs[0], jobs[0]])
+    with pytest.raises(pkg.FmxError):
+        ix.locate_group_async(dup)
+    ix.close()
