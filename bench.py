@@ -7,11 +7,15 @@ EncodingTable, SA sampling 2, k-mer table k = 3; 100,000 x 20 bp patterns cut
 from the text at uniform random starts (bench/src/generate.rs:105-113, cold
 ratio 1.0), per GPU.  `--config c1|c3|c4|c5` selects the other BASELINE configs.
 
-One step = one fmx_locate_batch_async call over the batch = one launch of the
-fused k_locate kernel: k-mer seed + LF loop, single-pass look-back scan of the
-counts into output offsets, locations — every count (as offsets) and every
-location of every pattern, written to HBM.  Inputs (text, blob, derived index
-structures, patterns) are resident in HBM before the timed region.
+One step = one full count+locate pass over one batch in the fused k_locate
+kernel: k-mer seed + LF loop, single-pass look-back scan of the counts into
+output offsets, locations — every count (as offsets) and every location of
+every pattern, written to that batch's own HBM outputs.  By default four
+steps' batches share one launch (fmx_locate_group_async; --group 1: one
+launch per batch) and launches alternate over two streams; 16 distinct
+batches are cycled so that no pass finds the previous pass's index lines in
+cache.  Inputs (text, blob, derived index structures, patterns) are resident
+in HBM before the timed region.
 
 Multi-GPU: one process per GPU (torchrun); each rank builds its own replica of
 the blob on its GPU (deterministic), runs its own pattern batch (weak scaling,
@@ -330,7 +334,7 @@ def main():
     if world > 1:
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        g_off, g_locs = D.concat_results(d_loff, d_locs[:need].to(torch.int64))
+        g_off, g_locs = D.concat_results(d_loff, d_locs[:int(d_need.item())].to(torch.int64))
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         log(f"[rank {rank}] gathered {g_off.numel() - 1:,} patterns / {g_locs.numel():,} locations in {gather_ms:.2f} ms")
