@@ -202,6 +202,36 @@ struct PatView {
     FMX_HD uint32_t at(uint64_t j) const { return sym ? sym[j] : enc[raw[rev ? m - 1 - j : j]]; }
 };
 
+// Four text symbols t[a..a+4) from two aligned words (the text buffer is
+// padded by 16 bytes past n).
+FMX_HD uint32_t load4(const uint8_t *t, uint64_t a) {
+    const uint64_t al = a & ~3ull;
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t *>(t + al);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(t + al + 4);
+    return sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+}
+
+// Single-row tail, short form (kernels for batches of short patterns): the
+// same contract as tail_mismatch_long below, four positions per step, inline
+// and register-light (most such tails are a few symbols long, or none).
+FMX_HD int64_t tail_mismatch_short(const uint8_t *text, const PatView &pv, uint64_t idx, uint64_t x, uint64_t top) {
+    const uint64_t lowest = idx > x ? idx - x : 0;  // positions below have no text before them
+    const uint64_t tb = x - idx;                     // text position of P[0] (mod 2^64)
+    uint64_t hj = top;
+    while (hj > lowest) {
+        const uint64_t lj = hj - lowest >= 4 ? hj - 4 : lowest;
+        const uint32_t tw = load4(text, tb + lj);
+        uint32_t mism = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+            if (lj + u < hj && ((tw >> (8 * u)) & 0xffu) != pv.at(lj + u)) mism |= 1u << u;
+        if (mism) return (int64_t)(lj + (31 - __builtin_clz(mism)));
+        hj = lj;
+    }
+    return lowest > 0 ? (int64_t)(lowest - 1) : -1;
+}
+
 // Single-row tail (FMX_OPT_TEXT): the interval of P[idx..m) is the one row
 // whose suffix starts at text position x, so P occurs at most once, at
 // x - idx.  The LF loop would consume P[idx-1], P[idx-2], ... and stop at the
@@ -213,9 +243,10 @@ struct PatView {
 // compared (top = idx: all of them).  Returns the highest position jm that
 // fails (-1: P occurs at x - idx).
 // One out-of-line copy (not one per kernel instantiation): it only touches
-// the text and the pattern.
-__host__ __device__ __noinline__ inline int64_t tail_mismatch(const uint8_t *text, PatView pv, uint64_t idx,
-                                                              uint64_t x, uint64_t top) {
+// the text and the pattern.  Its call costs the calling kernel registers, so
+// only the long-pattern kernel variants (LT) use it.
+__host__ __device__ __noinline__ inline int64_t tail_mismatch_long(const uint8_t *text, PatView pv, uint64_t idx,
+                                                                   uint64_t x, uint64_t top) {
     using V4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint64_t lowest = idx > x ? idx - x : 0;  // positions below have no text before them
     const uint64_t tb = x - idx;                     // text position of P[0] (mod 2^64)
@@ -256,6 +287,12 @@ __host__ __device__ __noinline__ inline int64_t tail_mismatch(const uint8_t *tex
     return lowest > 0 ? (int64_t)(lowest - 1) : -1;
 }
 
+template <bool LT>
+FMX_HD int64_t tail_mismatch(const uint8_t *text, const PatView &pv, uint64_t idx, uint64_t x, uint64_t top) {
+    if constexpr (LT) return tail_mismatch_long(text, pv, idx, x, top);
+    else return tail_mismatch_short(text, pv, idx, x, top);
+}
+
 // How a search ended (what the locate phase does with an occurrence):
 constexpr uint32_t kHitRows = 0;  // rows lo..hi of the final interval: walk (or read the full SA)
 constexpr uint32_t kHitOne = 1;   // resolved: the count is hi - lo <= 1 and rloc is the location
@@ -272,7 +309,7 @@ constexpr uint32_t kHitMask = 2;  // set bits b of `mask`: location SA[lo + b] -
 // suffixes at SA - idx sort as the suffixes at SA do.  This is the LF loop's
 // result over the same rows (with_slice.rs:27-31); callers only scan when no
 // symbol of P is >= sigma (which the LF loop would have to reject in place).
-template <typename P>
+template <typename P, bool LT>
 FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo, P &hi, P &rloc, uint64_t &mask,
                       uint32_t &mode) {
     const uint32_t W = a.sigma + 1, Cl = a.ctx_len;
@@ -325,7 +362,7 @@ FMX_HD void scan_rows(const QueryArgs &a, const PatView &pv, uint64_t idx, P &lo
         for (uint64_t m2 = msk; m2; m2 &= m2 - 1) {
             const uint64_t b = (uint64_t)__builtin_ctzll(m2);
             const P x = sa[2 * ((uint64_t)lo + b)];
-            if (tail_mismatch(a.text, pv, idx, (uint64_t)x, idx - Cl) < 0) {
+            if (tail_mismatch<LT>(a.text, pv, idx, (uint64_t)x, idx - Cl) < 0) {
                 if (!keep) first = x;
                 keep |= 1ull << b;
             }
@@ -359,7 +396,7 @@ FMX_HD constexpr P row_flag() { return P(1) << (8 * sizeof(P) - 1); }
 // position that does not — where it reads, and for PassThrough rejects, that
 // pattern symbol.  Here the nearest dlut_ctx positions are compared in one
 // XOR and the rest against the text.
-template <typename P>
+template <typename P, bool LT>
 FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w0, P w1, P &lo, P &hi, P &rloc,
                         uint32_t &mode) {
     const uint32_t bps = a.dlut_bps, Ld = a.dlut_ctx;
@@ -375,7 +412,7 @@ FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w
     const uint64_t diff = (pc ^ (uint64_t)(w0 & (P)~row_flag<P>())) & keep;
     int64_t jm;
     if (diff) jm = (int64_t)(idx - 1 - (uint64_t)__builtin_ctzll(diff) / bps);
-    else jm = idx > Ld ? tail_mismatch(a.text, pv, idx, x, idx - Ld) : -1;
+    else jm = idx > Ld ? tail_mismatch<LT>(a.text, pv, idx, x, idx - Ld) : -1;
     mode = kHitOne;
     lo = 0;
     hi = 0;
@@ -390,7 +427,7 @@ FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w
 // mode kHitRows, or (derived structures) an interval finished early: a
 // single row checked against the text (kHitOne), or a row-context scan
 // (kHitOne / kHitMask, see scan_rows).  The count is always hi - lo.
-template <typename P, int N, int VB, int REC>
+template <typename P, int N, int VB, int REC, bool LT = false>
 FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv, P &lo, P &hi, P &rloc,
                        uint64_t &mask, uint32_t &mode) {
     using O = Occ<P, N, VB, REC>;
@@ -425,7 +462,7 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
             const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
             const P w0 = dl[0], w1 = dl[1];
             idx = m - K;
-            if (a.dlut_rows && (w0 & row_flag<P>())) return one_row<P>(a, pv, idx, w0, w1, lo, hi, rloc, mode);
+            if (a.dlut_rows && (w0 & row_flag<P>())) return one_row<P, LT>(a, pv, idx, w0, w1, lo, hi, rloc, mode);
             lo = w0;
             hi = w1;
             seeded = true;
@@ -455,12 +492,12 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
     uint32_t c = idx > 0 ? pv.at(idx - 1) : 0;  // next symbol, fetched one step ahead
     while (lo < hi && idx > 0) {
         if (scan && hi - lo <= (P)a.scan_rows) {
-            scan_rows<P>(a, pv, idx, lo, hi, rloc, mask, mode);
+            scan_rows<P, LT>(a, pv, idx, lo, hi, rloc, mask, mode);
             return 0;
         }
         if (a.text != nullptr && hi - lo == P(1)) {
             const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[(uint64_t)lo * a.sa_stride];
-            const int64_t jm = tail_mismatch(a.text, pv, idx, x, idx);
+            const int64_t jm = tail_mismatch<LT>(a.text, pv, idx, x, idx);
             mode = kHitOne;
             if (jm >= 0) {
                 // the LF loop reads (and would reject) the symbol at jm before

@@ -144,7 +144,7 @@ __device__ __forceinline__ PatView pattern_view(const Tables<P> &s, const uint8_
     return pv;
 }
 
-template <typename P, int N, int VB, int REC>
+template <typename P, int N, int VB, int REC, bool LT>
 __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
                                                const uint64_t *__restrict__ offs, uint64_t npat,
                                                uint32_t flags, P *__restrict__ out_cnt, uint32_t stage_bytes) {
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
     P lo, hi, rloc;
     uint64_t mask;
     uint32_t mode;
-    const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
+    const uint32_t bad = search<P, N, VB, REC, LT>(a, s, pv, lo, hi, rloc, mask, mode);
     if (bad) atomicOr(a.status, bad);
     out_cnt[i] = hi - lo;
 }
@@ -223,8 +223,8 @@ __device__ __forceinline__ void emit_locations(const QueryArgs &a, const P *C, u
 // 1..kLocateEpochs per workspace and zeroes the used tiles before reusing 1.
 constexpr uint64_t kTileAgg = 1, kTileInc = 2;
 
-template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const LocateGroup grp, uint32_t stage_bytes) {
+template <typename P, int N, int VB, int REC, bool LT>
+__global__ __launch_bounds__(256, LT ? 4 : 8) void k_locate(const QueryArgs a, const LocateGroup grp, uint32_t stage_bytes) {
     __shared__ Tables<P> s;
     extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     __shared__ uint64_t s_scan[4];
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void k_locate(const QueryArgs a, const LocateG
     uint32_t mode = kHitRows;
     if (i < npat) {
         const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
-        const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
+        const uint32_t bad = search<P, N, VB, REC, LT>(a, s, pv, lo, hi, rloc, mask, mode);
         if (bad) atomicOr(a.status, bad);
         if (out_cnt) out_cnt[i] = hi - lo;
     }
@@ -678,8 +678,12 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
     if (n == 0) return hipSuccess;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         const uint32_t sb = stage_bytes_for(flags);
-        hipLaunchKernelGGL((k_count<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
-                           d_offsets, n, flags, (P *)d_counts, sb);
+        if (sb > (uint32_t)kStageBytes)  // long patterns: the vectorised tail compare
+            hipLaunchKernelGGL((k_count<P, N, VB, R, true>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
+                               d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
+        else
+            hipLaunchKernelGGL((k_count<P, N, VB, R, false>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
+                               d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
         return hipGetLastError();
     });
 }
@@ -698,7 +702,12 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
             grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles,
                                    epoch, (flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
             grp.n = 1;
-            hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, grp, sb);
+            if (sb > (uint32_t)kStageBytes)
+                hipLaunchKernelGGL((k_locate<P, N, VB, R, true>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
+                                   grp, sb);
+            else
+                hipLaunchKernelGGL((k_locate<P, N, VB, R, false>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
+                                   grp, sb);
             return hipGetLastError();
         }
         // workspace: [tile counts: tiles_cap][tile offsets: tiles_cap][records: n]
@@ -725,7 +734,12 @@ hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         const uint32_t sb = stage_bytes_for(stage_flags);
-        hipLaunchKernelGGL((k_locate<P, N, VB, R>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa, grp, sb);
+        if (sb > (uint32_t)kStageBytes)  // long patterns: the vectorised tail compare
+            hipLaunchKernelGGL((k_locate<P, N, VB, R, true>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa,
+                               grp, sb);
+        else
+            hipLaunchKernelGGL((k_locate<P, N, VB, R, false>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa,
+                               grp, sb);
         return hipGetLastError();
     });
 }

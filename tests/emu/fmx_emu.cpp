@@ -22,7 +22,8 @@ template <typename P, int N, int VB, int REC>
 int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
         uint32_t flags, uint64_t *counts, uint64_t *locs, uint64_t cap, uint64_t *needed) {
     const uint32_t scan_rows = options >> 8 ? options >> 8 : 32;  // options bits 8..: FMX_SCAN_ROWS
-    options &= 0xffu;
+    const bool long_tails = (options & 128u) != 0;
+    options &= 0x7fu;
     QueryArgs a{};
     const uint8_t *blob = ox.blob;
     a.ckpt = blob + ox.off_ckpt;
@@ -177,7 +178,9 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
             for (uint64_t j = 0; j < pv.m; ++j) staged[j] = pv.at(j);
             pv.sym = staged.data();
         }
-        const uint32_t bad = search<P, N, VB, REC>(a, t, pv, lo, hi, rloc, mask, mode);
+        // option bit 128: the long-pattern kernels' tail compare (LT)
+        const uint32_t bad = long_tails ? search<P, N, VB, REC, true>(a, t, pv, lo, hi, rloc, mask, mode)
+                                        : search<P, N, VB, REC, false>(a, t, pv, lo, hi, rloc, mask, mode);
         if (bad) return bad == kStatusEmpty ? ORC_E_EMPTY_PATTERN : ORC_E_SYMBOL;
         const uint64_t cnt = (uint64_t)(hi - lo);
         counts[i] = cnt;
