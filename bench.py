@@ -10,9 +10,9 @@ ratio 1.0), per GPU.  `--config c1|c3|c4|c5` selects the other BASELINE configs.
 One step = one full count+locate pass over one batch in the fused k_locate
 kernel: k-mer seed + LF loop, single-pass look-back scan of the counts into
 output offsets, locations — every count (as offsets) and every location of
-every pattern, written to that batch's own HBM outputs.  By default four
+every pattern, written to that batch's own HBM outputs.  By default eight
 steps' batches share one launch (fmx_locate_group_async; --group 1: one
-launch per batch) and launches alternate over two streams; 16 distinct
+launch per batch) and launches alternate over two streams; 32 distinct
 batches are cycled so that no pass finds the previous pass's index lines in
 cache.  Inputs (text, blob, derived index structures, patterns) are resident
 in HBM before the timed region.
@@ -100,7 +100,7 @@ def phase_stamps(pkg, ix, step, B, out_path):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=800)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--text-len", type=int, default=0, help="override the config's text length")
@@ -117,7 +117,7 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no HIP events around the launches in the timed region (no roofline)")
     ap.add_argument("--count-only", action="store_true", help="diagnostic: time fmx_count_batch_async (k_count)")
-    ap.add_argument("--event-every", type=int, default=10,
+    ap.add_argument("--event-every", type=int, default=5,
                     help="bracket every k-th launch of the timed region with HIP events (an event pair costs the "
                          "stream several us; 1 = every launch)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
@@ -127,9 +127,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="launches in flight: launch q runs on HIP stream q %% S (each stream its own batches: "
                          "patterns, outputs and look-back workspaces), as a serving loop pipelines batches")
-    ap.add_argument("--batches", type=int, default=16,
+    ap.add_argument("--batches", type=int, default=32,
                     help="distinct pattern batches cycled over the steps (at least --streams)")
-    ap.add_argument("--group", type=int, default=4,
+    ap.add_argument("--group", type=int, default=8,
                     help="batches per kernel launch in the timed region (fmx_locate_group_async, at most 8; "
                          "1 = one launch per batch)")
     ap.add_argument("--submit", default="native", choices=["native", "python"],
