@@ -258,7 +258,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         }
     }
     ix->options = ix->occ_mode;
-    if (const char *env = getenv("FMX_LOCATE_SPLIT")) ix->locate_fused = atoi(env) == 0;
+    if (const char *env = getenv("FMX_LOCATE_FUSED")) ix->locate_fused = atoi(env) != 0;
     // deep-table digits: the symbols that occur in the text (a pattern holding
     // any other symbol is left to the blob's seed and the LF loop)
     uint32_t S = 0;
@@ -653,17 +653,6 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
         for (uint64_t k = 0; k < i; ++k)
             if (jobs[k].d_workspace == j.d_workspace) return FMX_E_ARG;  // one look-back per workspace
     }
-    if (!ix->locate_fused) {  // the split kernels: one batch after another
-        for (uint64_t i = 0; i < n_jobs; ++i) {
-            const fmx_locate_job &j = jobs[i];
-            const fmx_status st =
-                fmx_locate_batch_async(ix, j.d_bytes, j.d_offsets, j.n_patterns, j.flags, j.d_counts,
-                                       j.d_loc_offsets, j.d_locs, j.cap, j.d_needed, j.d_workspace,
-                                       j.workspace_bytes, s);
-            if (st) return st;
-        }
-        return FMX_OK;
-    }
     // up to kMaxGroup non-empty batches per launch; empty ones get their
     // zero offset and total directly
     uint64_t i = 0;
@@ -680,8 +669,8 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
                 continue;
             }
             const uint64_t G = locate_tiles_cap(j.n_patterns);
-            uint32_t epoch = 0;
-            if (next_epoch(ix, j.d_workspace, G, s, &epoch) != FMX_OK) return FMX_E_DEVICE;
+            uint32_t epoch = 1;  // (the split kernels need none)
+            if (ix->locate_fused && next_epoch(ix, j.d_workspace, G, s, &epoch) != FMX_OK) return FMX_E_DEVICE;
             grp.tile_begin[grp.n] = tiles;
             grp.b[grp.n++] = LocateBatch{j.d_bytes, j.d_offsets, j.n_patterns, j.d_counts, j.d_loc_offsets,
                                          j.d_locs, j.cap, j.d_needed, (uint64_t *)((uint8_t *)j.d_workspace + 256),

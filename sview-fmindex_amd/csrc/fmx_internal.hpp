@@ -121,7 +121,8 @@ struct fmx_index {
     uint64_t safull_bytes = 0;
     uint8_t *d_text = nullptr;
     uint32_t options = 0;
-    bool locate_fused = true;  // FMX_LOCATE_SPLIT=1: k_search + k_emit instead of k_locate (A/B)
+    bool locate_fused = false;  // FMX_LOCATE_FUSED=1: the single-kernel k_locate (look-back) instead of
+                                // k_search + k_scan + k_emit
     fmx::QueryArgs qa{};
     // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
@@ -150,8 +151,8 @@ namespace fmx {
 // Query launchers (fmx_query.hip).  All asynchronous on `stream`.
 hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                         uint32_t flags, void *d_counts, hipStream_t stream);
-// Count + offsets scan + locate: the fused k_locate (or k_search then k_emit
-// with FMX_LOCATE_SPLIT=1).  d_ctl (2 x u32) and d_tiles must be zero before
+// Count + offsets scan + locate: k_search, k_scan, k_emit (or, with
+// FMX_LOCATE_FUSED=1, the single-kernel k_locate).  d_ctl (2 x u32) and d_tiles must be zero before
 // their first use.  k_locate: d_tiles holds tiles_cap epoch-tagged look-back
 // words, epoch in 1..kLocateEpochs (fmx_api.cpp hands them out per workspace);
 // split: d_tiles = [tile counts][tile offsets][n search records], d_ctl its

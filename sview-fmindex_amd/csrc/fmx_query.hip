@@ -390,27 +390,42 @@ __device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &
     return is_mask ? (uint64_t)__builtin_popcountll(x) : (uint64_t)r.b;
 }
 
-// Phase 1 of a locate batch: the search of every pattern (no waiting on other
-// workgroups), its result record, and the tile's count.  The last workgroup
-// to finish (agent-scope counter) turns the tile counts into exclusive tile
-// offsets and the batch total, so k_emit needs no look-back.
-template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_search(const QueryArgs a, const uint8_t *__restrict__ bytes,
-                                                const uint64_t *__restrict__ offs, uint64_t npat, uint32_t flags,
-                                                P *__restrict__ out_cnt, SearchRec<P> *__restrict__ recs,
-                                                uint64_t *__restrict__ tile_cnt, uint64_t *__restrict__ tile_off,
-                                                uint32_t *__restrict__ ctl, uint64_t *__restrict__ loc_off,
-                                                uint64_t *__restrict__ needed, uint32_t stage_bytes) {
+// The three-kernel locate (the default; FMX_LOCATE_FUSED=1 selects k_locate).
+// No workgroup ever waits on another, so nothing depends on the order or
+// placement in which workgroups are dispatched (MI355X_MICROARCH.md: HIP
+// promises neither; a look-back that assumes in-order dispatch can deadlock
+// when launches on several streams share the CUs).  Per batch of a group:
+// workspace = [256 B][tile counts: G][tile offsets: G][search records: n].
+
+// This workgroup's batch of a grouped launch (workgroup-uniform).
+__device__ __forceinline__ uint32_t group_batch(const LocateGroup &grp) {
+    uint32_t jb = 0;
+#pragma unroll
+    for (uint32_t t = 1; t < kMaxGroup; ++t)
+        if (t < grp.n && blockIdx.x >= grp.tile_begin[t]) jb = t;
+    return jb;
+}
+
+// 1. Search every pattern; its result record, its count; the tile's count.
+template <typename P, int N, int VB, int REC, bool LT>
+__global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
+                                                             uint32_t stage_bytes) {
     __shared__ Tables<P> s;
     extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
     __shared__ uint64_t s_scan[4];
-    __shared__ uint32_t s_last;
     stage_tables(a, s);
-    const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
-    const uint32_t G = (uint32_t)((npat + 255) / 256), g = blockIdx.x;
+    const uint32_t jb = group_batch(grp);
+    const LocateBatch &B = grp.b[jb];
+    const uint8_t *__restrict__ bytes = B.bytes;
+    const uint64_t *__restrict__ offs = B.offs;
+    const uint64_t npat = B.npat;
+    const bool rev = B.rev != 0;
+    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
+    const uint64_t G = (npat + 255) / 256;
+    SearchRec<P> *__restrict__ recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
     uint64_t beg, end, b0, b1;
-    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end,
-                                       b0, b1);
+    const bool staged =
+        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end, b0, b1);
     __syncthreads();
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     uint64_t cnt = 0;
@@ -419,31 +434,33 @@ __global__ __launch_bounds__(256) void k_search(const QueryArgs a, const uint8_t
         P lo, hi, rloc;
         uint64_t mask;
         uint32_t mode;
-        const uint32_t bad = search<P, N, VB, REC>(a, s, pv, lo, hi, rloc, mask, mode);
+        const uint32_t bad = search<P, N, VB, REC, LT>(a, s, pv, lo, hi, rloc, mask, mode);
         if (bad) atomicOr(a.status, bad);
         cnt = (uint64_t)(hi - lo);
-        if (out_cnt) out_cnt[i] = hi - lo;
+        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = hi - lo;
         recs[i] = pack_rec<P>(lo, hi, rloc, mask, mode);
     }
     uint64_t agg;
     block_excl_scan(cnt, &agg, s_scan);
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&tile_cnt[g], agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t done = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = done == G - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // The last workgroup: exclusive scan of the G tile counts, 16 per thread
-    // per pass (every load of a pass in flight at once).
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (threadIdx.x == 0) B.tiles[g] = agg;
+}
+
+// 2. One workgroup per batch: exclusive scan of its tile counts into tile
+// offsets, and the batch total (16 tiles per thread per pass, every load of
+// a pass in flight at once).
+__global__ __launch_bounds__(256) void k_scan(const LocateGroup grp) {
+    __shared__ uint64_t s_scan[4];
+    const LocateBatch &B = grp.b[blockIdx.x];
+    const uint64_t G = (B.npat + 255) / 256;
+    const uint64_t *cnt = B.tiles;
+    uint64_t *off = B.tiles + G;
     uint64_t carry = 0;
     for (uint64_t base = 0; base < G; base += 256 * 16) {
         uint64_t v[16], sum = 0;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const uint64_t t = base + threadIdx.x * 16ull + u;
-            v[u] = t < G ? __hip_atomic_load(&tile_cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            v[u] = t < G ? cnt[t] : 0;
             sum += v[u];
         }
         uint64_t tot;
@@ -451,37 +468,57 @@ __global__ __launch_bounds__(256) void k_search(const QueryArgs a, const uint8_t
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             const uint64_t t = base + threadIdx.x * 16ull + u;
-            if (t < G) tile_off[t] = run;
+            if (t < G) off[t] = run;
             run += v[u];
         }
         carry += tot;
     }
     if (threadIdx.x == 0) {
-        loc_off[npat] = carry;
-        *needed = carry;
-        __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+        B.loc_off[B.npat] = carry;
+        *B.needed = carry;
     }
 }
 
-// Phase 2: output offsets (tile offset + in-tile scan) and every location,
-// rows dealt across each wave's lanes (emit_locations).
+// 3. Output offsets (tile offset + in-tile scan) and every location, rows
+// dealt across each wave's lanes (emit_locations).
+// fold: batches of at most kFoldTiles tiles need no k_scan: each workgroup
+// sums the counts of the tiles before its own (all final: k_search is done),
+// and the last tile writes the batch total.
+constexpr uint64_t kFoldTiles = 2048;
+
 template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_emit(const QueryArgs a, uint64_t npat, const SearchRec<P> *__restrict__ recs,
-                                              const uint64_t *__restrict__ tile_off, uint64_t *__restrict__ loc_off,
-                                              P *__restrict__ out_locs, uint64_t cap) {
+__global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGroup grp, uint32_t fold) {
     __shared__ P sC[kMaxSigma + 1];
     __shared__ uint64_t s_scan[4];
     if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
-    const uint64_t g = blockIdx.x, i = g * 256u + threadIdx.x;
+    const uint32_t jb = group_batch(grp);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t npat = B.npat, G = (npat + 255) / 256;
+    const uint64_t g = blockIdx.x - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
+    const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
     P lo = 0, rloc = 0;
     uint64_t mask = 0, cnt = 0;
     uint32_t mode = kHitOne;
     if (i < npat) cnt = unpack_rec<P>(recs[i], lo, rloc, mask, mode);
-    const uint64_t base = tile_off[g];
+    uint64_t base;
+    if (fold) {
+        uint64_t part = 0;
+        for (uint64_t t = threadIdx.x; t < g; t += 256) part += B.tiles[t];
+        uint64_t tot;
+        block_excl_scan(part, &tot, s_scan);
+        base = tot;
+    } else {
+        base = B.tiles[G + g];
+    }
     uint64_t agg;
     const uint64_t my_off = base + block_excl_scan(cnt, &agg, s_scan);  // (its barriers publish sC)
-    if (i < npat) loc_off[i] = my_off;
-    emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, cap, out_locs);
+    if (fold && g == G - 1 && threadIdx.x == 0) {
+        B.loc_off[npat] = base + agg;
+        *B.needed = base + agg;
+    }
+    if (i < npat) B.loc_off[i] = my_off;
+    emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, B.cap,
+                                  reinterpret_cast<P *>(B.out_locs));
 }
 
 // ------------------------------------------------------------ deep k-mer table
@@ -688,6 +725,21 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
     });
 }
 
+// The three kernels of a (grouped) split locate, one after another on `stream`.
+template <typename P, int N, int VB, int R>
+static hipError_t launch_split(const fmx_index *ix, const LocateGroup &grp, uint32_t tiles, uint32_t sb,
+                               hipStream_t stream) {
+    if (sb > (uint32_t)kStageBytes)
+        hipLaunchKernelGGL((k_search<P, N, VB, R, true>), dim3(tiles), dim3(256), sb, stream, ix->qa, grp, sb);
+    else
+        hipLaunchKernelGGL((k_search<P, N, VB, R, false>), dim3(tiles), dim3(256), sb, stream, ix->qa, grp, sb);
+    uint32_t fold = 1;
+    for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
+    if (!fold) hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
+    hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(tiles), dim3(256), 0, stream, ix->qa, grp, fold);
+    return hipGetLastError();
+}
+
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                          uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
                          uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
@@ -710,15 +762,11 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                                    grp, sb);
             return hipGetLastError();
         }
-        // workspace: [tile counts: tiles_cap][tile offsets: tiles_cap][records: n]
-        uint64_t *tile_cnt = d_tiles, *tile_off = d_tiles + tiles_cap;
-        SearchRec<P> *recs = reinterpret_cast<SearchRec<P> *>(d_tiles + 2 * tiles_cap);
-        hipLaunchKernelGGL((k_search<P, N, VB, R>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa, d_bytes,
-                           d_offsets, n, flags, (P *)d_counts, recs, tile_cnt, tile_off, d_ctl, d_loc_offsets,
-                           d_needed, sb);
-        hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(grid_for(n)), dim3(256), 0, stream, ix->qa, n,
-                           (const SearchRec<P> *)recs, (const uint64_t *)tile_off, d_loc_offsets, (P *)d_locs, cap);
-        return hipGetLastError();
+        LocateGroup grp{};
+        grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles, 1u,
+                               (flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
+        grp.n = 1;
+        return launch_split<P, N, VB, R>(ix, grp, (uint32_t)((n + 255) / 256), sb, stream);
     });
 }
 
@@ -728,12 +776,13 @@ hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint
     uint64_t tiles = 0;
     for (uint32_t j = 0; j < grp.n; ++j) {
         if (grp.b[j].npat == 0 || grp.tile_begin[j] != tiles) return hipErrorInvalidValue;
-        if (grp.b[j].epoch == 0 || grp.b[j].epoch > kLocateEpochs) return hipErrorInvalidValue;
+        if (ix->locate_fused && (grp.b[j].epoch == 0 || grp.b[j].epoch > kLocateEpochs)) return hipErrorInvalidValue;
         tiles += (grp.b[j].npat + 255) / 256;
     }
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
         const uint32_t sb = stage_bytes_for(stage_flags);
+        if (!ix->locate_fused) return launch_split<P, N, VB, R>(ix, grp, (uint32_t)tiles, sb, stream);
         if (sb > (uint32_t)kStageBytes)  // long patterns: the vectorised tail compare
             hipLaunchKernelGGL((k_locate<P, N, VB, R, true>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa,
                                grp, sb);

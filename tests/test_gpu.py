@@ -481,3 +481,26 @@ def test_locate_group_launch(pkg, O):
     with pytest.raises(pkg.FmxError):
         ix.locate_group_async(dup)
     ix.close()
+
+
+def test_large_batch_scan_kernel(pkg, O):
+    """A batch of more than 2048 tiles (524,288 patterns): its tile offsets
+    come from the separate k_scan kernel instead of k_emit's own sum."""
+    rng = np.random.default_rng(44)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=60_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    n = 600_000
+    lens = rng.integers(3, 13, size=n)
+    starts = rng.integers(0, text.size - 13, size=n)
+    idx = starts[:, None] + np.arange(12)[None, :]
+    rows = text[idx]
+    data = np.concatenate([rows[i, :lens[i]] for i in range(n)]).astype(np.uint8)
+    offsets = np.zeros(n + 1, np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ooff, olocs = orc.locate_batch(data, offsets, threads=8)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    goff, glocs = ix.locate_batch((data, offsets))
+    assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    ix.close()
