@@ -354,7 +354,7 @@ def main():
     kern = {name: t["total_ms"] / max(t["launches"], 1) for name, t in timing.items()}
     if "locate" not in kern:  # --no-kernel-timing
         kern["locate"] = float("nan")
-    dominant = "locate"   # the single fused launch of a step (k_locate)
+    dominant = "locate"   # one grouped launch: k_search + k_emit (+ k_scan), or the fused k_locate
     if args.count_only:
         dominant = "count"
         kern.pop("locate", None)
@@ -366,6 +366,8 @@ def main():
     achieved = alg_bytes / (kern[dominant] * 1e-3) / 1e9
     traffic, traffic_src = None, None
     key = f"{args.config}:{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}" + (f":g{GR}" if native and GR > 1 else "")
+    if os.environ.get("FMX_LOCATE_FUSED", "0") not in ("", "0"):
+        key += ":fused"
     if os.path.exists(args.traffic_json):
         try:
             pm = json.load(open(args.traffic_json))

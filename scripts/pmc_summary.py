@@ -29,7 +29,8 @@ def bench_line(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="k_locate")
+    ap.add_argument("--kernel", default="k_search,k_scan,k_emit,k_locate",
+                    help="comma-separated kernel names making up one locate step; per-dispatch means are summed")
     ap.add_argument("--json", default=os.path.join(ROOT, "profiles", "pmc_fetch_size.json"))
     args = ap.parse_args()
     b = bench_line(os.path.join(OUT, f"{args.tag}_trace.log"))
@@ -37,23 +38,40 @@ def main():
     run = {"counters": {}}
     name = None
     durations = []
+    kernels = [k for k in args.kernel.split(",") if k]
+
+    def which(kname):
+        for k in kernels:
+            if f"fmx::{k}<" in kname or f"fmx::{k}(" in kname:
+                return k
+        return None
+
+    names = set()
     for d in sorted(glob.glob(os.path.join(OUT, f"{args.tag}_pmc*"))):
         f = os.path.join(d, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
-        per = defaultdict(lambda: defaultdict(float))
+        per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # counter -> kernel -> dispatch
         for r in csv.DictReader(open(f)):
-            if args.kernel not in r["Kernel_Name"]:
+            k = which(r["Kernel_Name"])
+            if k is None:
                 continue
-            name = r["Kernel_Name"]
-            per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
-        for cn, by in per.items():
-            run["counters"][cn] = {"launches": len(by), "mean_per_launch": sum(by.values()) / len(by)}
+            names.add(r["Kernel_Name"])
+            per[r["Counter_Name"]][k][r["Dispatch_Id"]] += float(r["Counter_Value"])
+        for cn, byk in per.items():
+            # one locate step = one dispatch of each of its kernels: sum the per-kernel means
+            launches = max(len(by) for by in byk.values())
+            run["counters"][cn] = {"launches": launches,
+                                   "mean_per_launch": sum(sum(by.values()) / len(by) for by in byk.values())}
     stats = os.path.join(OUT, f"{args.tag}_trace", "run_kernel_stats.csv")
+    avg, calls = 0.0, 0
     for r in csv.DictReader(open(stats)):
-        if args.kernel in r["Name"]:
-            run["avg_duration_ns"] = float(r["AverageNs"])
-            run["launches"] = int(r["Calls"])
+        if which(r["Name"]):
+            avg += float(r["AverageNs"])
+            calls = max(calls, int(r["Calls"]))
+    run["avg_duration_ns"] = avg  # summed over the step's kernels
+    run["launches"] = calls
+    name = " + ".join(sorted(names))
     run["kernel"] = name
     c = run["counters"]
     if "FETCH_SIZE" in c:
