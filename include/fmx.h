@@ -188,10 +188,14 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
 fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
                                  uint64_t n_patterns, uint32_t flags, void *d_counts, void *stream);
 
-/* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns.
- * A workspace is zeroed by the caller before its first use, then belongs to
- * this index: its launches are ordered on one stream at a time (the index
- * tracks a look-back epoch per workspace address and clears what it needs). */
+/* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
+ * [256 B][tile counts][tile offsets][one search record per pattern].  A
+ * workspace is zeroed by the caller before its first use, then belongs to
+ * this index: its launches are ordered on one stream at a time.  (The
+ * default locate is k_search + k_emit, which never makes one workgroup wait
+ * on another; with FMX_LOCATE_FUSED=1 in the environment the single-kernel
+ * k_locate is used instead, and the index tracks a look-back epoch per
+ * workspace address and clears what it needs.) */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)
