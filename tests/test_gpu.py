@@ -504,3 +504,20 @@ def test_large_batch_scan_kernel(pkg, O):
     goff, glocs = ix.locate_batch((data, offsets))
     assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
     ix.close()
+
+
+@pytest.mark.parametrize("pb,planes,vb", [(4, 3, 64), (8, 3, 128), (4, 5, 32), (8, 2, 64)])
+def test_fused_locate_kernel(pkg, O, pb, planes, vb, monkeypatch):
+    """FMX_LOCATE_FUSED=1 (the single-kernel k_locate with its look-back):
+    same results as the oracle, for short and long patterns, every load
+    option set; and grouped launches through it."""
+    monkeypatch.setenv("FMX_LOCATE_FUSED", "1")
+    rng = np.random.default_rng(pb * 7 + planes * 3 + vb)
+    chars = rand_chr_list(rng, 4)
+    table = table_from_symbols([bytes([c]) for c in chars])
+    text = rand_text(rng, chars, 30000, 30000)
+    blob = gpu_build(pkg, text, 4, pb, planes, vb, 3, 2, table)
+    pats = [rand_pattern(rng, text, 1, 24) for _ in range(1500)]
+    pats += [rand_pattern(rng, text, 70, 160) for _ in range(300)]  # the long-pattern variant's staging
+    for occ in (1, 4 | 8, 63):
+        check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, reversed_too=(occ == 63))
