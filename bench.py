@@ -123,6 +123,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (1 thread)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
+    ap.add_argument("--no-fixed-len", action="store_true",
+                    help="A/B: do not pass FMX_HINT_FIXED_LEN (the kernels read each tile's offsets first)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--streams", type=int, default=2,
                     help="launches in flight: launch q runs on HIP stream q %% S (each stream its own batches: "
@@ -247,22 +249,23 @@ def main():
     d_cnt = torch.zeros(B, dtype=pdt_t, device=dev)
 
     stage_kb = min(56, -(-256 * m // 1024))  # FMX_HINT_STAGE_KB: every tile spans 256 * m bytes
+    fixed = 0 if args.no_fixed_len else m    # FMX_HINT_FIXED_LEN: every pattern is m bytes (checked on device)
 
     def job(bt):
         return ix.locate_job(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, bt["loff"].data_ptr(),
                              bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
-                             stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
+                             stream=bt["stream"].cuda_stream, stage_kb=stage_kb, fixed_len=fixed)
 
     def step():
         bt = batches[state["i"] % NB]
         state["i"] += 1
         if args.count_only:  # diagnostic: the search alone (k_count)
             ix.count_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, d_cnt.data_ptr(),
-                                 stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
+                                 stream=bt["stream"].cuda_stream, stage_kb=stage_kb, fixed_len=fixed)
             return
         ix.locate_batch_async(bt["pat"].data_ptr(), bt["off"].data_ptr(), B, bt["loff"].data_ptr(),
                               bt["locs"].data_ptr(), cap, bt["need"].data_ptr(), bt["ws"].data_ptr(), ws,
-                              stream=bt["stream"].cuda_stream, stage_kb=stage_kb)
+                              stream=bt["stream"].cuda_stream, stage_kb=stage_kb, fixed_len=fixed)
 
     # native submission: the K steps of the timed region as ceil(K / GR)
     # grouped launches (GR = 1: one queue of K single-batch jobs)
@@ -420,7 +423,7 @@ def main():
             "load_options": info["options"], "deep_lut_k": info["deep_lut_k"],
             "index_hbm_bytes": info["device_bytes"],
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
-            "streams": S, "batches_per_launch": GR if native else 1, "distinct_batches": NB, "submit": "native" if native else "python",
+            "streams": S, "fixed_len_hint": fixed, "batches_per_launch": GR if native else 1, "distinct_batches": NB, "submit": "native" if native else "python",
         },
         "roofline": {
             "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

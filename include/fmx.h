@@ -68,6 +68,13 @@ typedef struct fmx_layout {
  * HBM instead (same results).  Less LDS per workgroup = more workgroups per
  * CU.  Overrides FMX_HINT_LONG_PATTERNS; the host-buffer calls set it exactly. */
 #define FMX_HINT_STAGE_KB(kb) ((((uint32_t)(kb)) & 0xffu) << 8)
+/* Performance hint: every pattern is m bytes (1..65535) and d_offsets[i] ==
+ * i * m, so the kernels address each pattern's bytes without first reading
+ * the offsets (one dependent HBM round trip fewer per workgroup).  The
+ * offsets are still read alongside and checked: a batch that disagrees is
+ * reported as FMX_E_ARG (its outputs are then undefined).  The host-buffer
+ * calls set it themselves when every pattern has the same length. */
+#define FMX_HINT_FIXED_LEN(m) ((((uint32_t)(m)) & 0xffffu) << 16)
 
 /* Load options: device-side structures derived from the blob at load time.
  * Results are identical with any combination; they trade HBM for fewer

@@ -324,11 +324,15 @@ def _options(occ: str, deep_lut: bool, full_sa: bool = True, text: bool = True, 
             | (_n.FMX_OPT_LUT_ROWS if lut_rows else 0))
 
 
-def _flags(reversed: bool, long_patterns: bool, stage_kb: int = 0) -> int:
-    """Query flags: FMX_PATTERN_REVERSED, FMX_HINT_LONG_PATTERNS, and
-    FMX_HINT_STAGE_KB(stage_kb) (LDS KB per 256-pattern tile; 0 = no hint)."""
+def _flags(reversed: bool, long_patterns: bool, stage_kb: int = 0, fixed_len: int = 0) -> int:
+    """Query flags: FMX_PATTERN_REVERSED, FMX_HINT_LONG_PATTERNS,
+    FMX_HINT_STAGE_KB(stage_kb) (LDS KB per 256-pattern tile; 0 = no hint) and
+    FMX_HINT_FIXED_LEN(fixed_len) (every pattern fixed_len bytes, offsets[i] ==
+    i * fixed_len; 0 = no hint)."""
+    if not 0 <= int(fixed_len) <= 0xFFFF:
+        raise ValueError("fixed_len must be in 0..65535")
     return ((_n.FMX_PATTERN_REVERSED if reversed else 0) | (_n.FMX_HINT_LONG_PATTERNS if long_patterns else 0)
-            | ((int(stage_kb) & 0xFF) << 8))
+            | ((int(stage_kb) & 0xFF) << 8) | (int(fixed_len) << 16))
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -532,8 +536,9 @@ class FmIndex:
 
     # -- device-resident API (pointers are ints; stream is a hipStream_t) --
     def count_batch_async(self, d_bytes: int, d_offsets: int, n: int, d_counts: int,
-                          stream: int = 0, reversed: bool = False, long_patterns: bool = False, stage_kb: int = 0) -> None:
-        flags = _flags(reversed, long_patterns, stage_kb)
+                          stream: int = 0, reversed: bool = False, long_patterns: bool = False, stage_kb: int = 0,
+                          fixed_len: int = 0) -> None:
+        flags = _flags(reversed, long_patterns, stage_kb, fixed_len)
         _check(_n.lib().fmx_count_batch_async(self._h, C.c_void_p(d_bytes), C.c_void_p(d_offsets), n, flags,
                                               C.c_void_p(d_counts), C.c_void_p(stream) if stream else None))
 
@@ -545,9 +550,10 @@ class FmIndex:
     def locate_batch_async(self, d_bytes: int, d_offsets: int, n: int, d_loc_offsets: int,
                            d_locs: int, cap: int, d_needed: int, d_ws: int, ws_bytes: int,
                            d_counts: int = 0, stream: int = 0, reversed: bool = False,
-                           long_patterns: bool = False, stage_kb: int = 0) -> None:
-        """`long_patterns`: FMX_HINT_LONG_PATTERNS (patterns average > 64 bytes)."""
-        flags = _flags(reversed, long_patterns, stage_kb)
+                           long_patterns: bool = False, stage_kb: int = 0, fixed_len: int = 0) -> None:
+        """`long_patterns`: FMX_HINT_LONG_PATTERNS (patterns average > 64 bytes);
+        `fixed_len`: FMX_HINT_FIXED_LEN (checked on the device: FMX_E_ARG at sync)."""
+        flags = _flags(reversed, long_patterns, stage_kb, fixed_len)
         _check(_n.lib().fmx_locate_batch_async(
             self._h, C.c_void_p(d_bytes), C.c_void_p(d_offsets), n, flags,
             C.c_void_p(d_counts) if d_counts else None, C.c_void_p(d_loc_offsets), C.c_void_p(d_locs), cap,
@@ -557,10 +563,11 @@ class FmIndex:
     @staticmethod
     def locate_job(d_bytes: int, d_offsets: int, n: int, d_loc_offsets: int, d_locs: int, cap: int,
                    d_needed: int, d_ws: int, ws_bytes: int, d_counts: int = 0, stream: int = 0,
-                   reversed: bool = False, long_patterns: bool = False, stage_kb: int = 0) -> "_n.fmx_locate_job":
+                   reversed: bool = False, long_patterns: bool = False, stage_kb: int = 0,
+                   fixed_len: int = 0) -> "_n.fmx_locate_job":
         """One entry of a locate queue (fmx_locate_job): the arguments of
         locate_batch_async."""
-        flags = _flags(reversed, long_patterns, stage_kb)
+        flags = _flags(reversed, long_patterns, stage_kb, fixed_len)
         return _n.fmx_locate_job(d_bytes, d_offsets, n, flags, 0, d_counts or None, d_loc_offsets, d_locs, cap,
                                  d_needed, d_ws, ws_bytes, stream or None)
 

@@ -342,6 +342,7 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
     if (st & kStatusHang) return FMX_E_DEVICE;
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
+    if (st & kStatusStride) return FMX_E_ARG;
     return FMX_OK;
 }
 
@@ -674,7 +675,7 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
             grp.tile_begin[grp.n] = tiles;
             grp.b[grp.n++] = LocateBatch{j.d_bytes, j.d_offsets, j.n_patterns, j.d_counts, j.d_loc_offsets,
                                          j.d_locs, j.cap, j.d_needed, (uint64_t *)((uint8_t *)j.d_workspace + 256),
-                                         epoch, (j.flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
+                                         epoch, (j.flags & FMX_PATTERN_REVERSED) ? 1u : 0u, j.flags >> 16};
             tiles += (uint32_t)G;
             units += j.n_patterns;
             // the launch stages with the largest hint of its batches
@@ -707,13 +708,18 @@ static fmx_status check_patterns(const uint64_t *offsets, uint64_t n) {
     return FMX_OK;
 }
 
-// FMX_HINT_STAGE_KB for a host batch: the most bytes any 256-pattern tile
-// spans, rounded up to whole KB (tiles past 56 KB read their patterns from HBM).
+// The hints for a host batch (they replace the caller's): FMX_HINT_STAGE_KB
+// = the most bytes any 256-pattern tile spans, rounded up to whole KB (tiles
+// past 56 KB read their patterns from HBM), and FMX_HINT_FIXED_LEN when every
+// pattern has the same length.
 static uint32_t stage_hint(const uint64_t *offsets, uint64_t n) {
     uint64_t most = 0;
     for (uint64_t t = 0; t < n; t += 256) most = std::max(most, offsets[std::min(n, t + 256)] - offsets[t]);
     const uint64_t kb = std::min<uint64_t>(std::max<uint64_t>((most + 1023) / 1024, 1), kStageBytesLong / 1024);
-    return FMX_HINT_STAGE_KB(kb);
+    const uint64_t m = offsets[1] - offsets[0];
+    bool fixed = m <= 0xffffu;
+    for (uint64_t i = 1; fixed && i < n; ++i) fixed = offsets[i + 1] - offsets[i] == m;
+    return FMX_HINT_STAGE_KB(kb) | (fixed ? FMX_HINT_FIXED_LEN(m) : 0u);
 }
 
 fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *offsets, uint64_t n,
@@ -733,7 +739,7 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return FMX_E_DEVICE;
-    flags |= stage_hint(offsets, n);
+    flags = (flags & 0xffu) | stage_hint(offsets, n);
     st = fmx_count_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, d + o_cnt, s);
     if (st) return st;
     if (hipMemcpyAsync(out_counts, d + o_cnt, n * pb, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
@@ -769,7 +775,7 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
     if (st) return st;
     hipSetDevice(ix->device);
     const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
-    flags |= stage_hint(offsets, n);
+    flags = (flags & 0xffu) | stage_hint(offsets, n);
     st = ensure_ws(ix, n);
     if (st) return st;
     const uint64_t o_off = align_up(nb, 256);

@@ -90,6 +90,7 @@ constexpr uint8_t kNoDigit = 0xFF;
 constexpr uint32_t kStatusEmpty = 1u;
 constexpr uint32_t kStatusSymbol = 2u;
 constexpr uint32_t kStatusHang = 4u;  // a bounded look-back spin gave up
+constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
 
 struct Timer {
     std::string name;
@@ -177,6 +178,7 @@ struct LocateBatch {
     uint64_t *tiles;
     uint32_t epoch;
     uint32_t rev;
+    uint32_t stride;  // FMX_HINT_FIXED_LEN: offs[i] == i * stride (0: read the offsets)
 };
 struct LocateGroup {
     LocateBatch b[kMaxGroup];

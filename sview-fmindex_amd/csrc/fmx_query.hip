@@ -87,14 +87,27 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total,
 template <typename P>
 __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
                                                const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
-                                               uint32_t stage_bytes, uint64_t &beg, uint64_t &end, uint64_t &b0,
-                                               uint64_t &b1) {
+                                               uint32_t stage_bytes, uint32_t stride, uint32_t *status,
+                                               uint64_t &beg, uint64_t &end, uint64_t &b0, uint64_t &b1) {
     const uint64_t last = first + 256 < npat ? first + 256 : npat;
     const uint64_t i = first + threadIdx.x;
-    b0 = offs[first];
-    b1 = offs[last];
-    beg = i < npat ? offs[i] : 0;
-    end = i < npat ? offs[i + 1] : 0;
+    uint64_t chk = 0;
+    if (stride) {
+        // FMX_HINT_FIXED_LEN: offs[i] == i * stride, so the byte loads need
+        // not wait for the offsets; each thread's own end offset is loaded
+        // alongside them and checked once they have arrived.
+        b0 = first * stride;
+        b1 = last * stride;
+        beg = i < npat ? i * stride : 0;
+        end = i < npat ? beg + stride : 0;
+        chk = i < npat ? offs[i + 1] : 0;
+        if (i == 0 && offs[0] != 0) atomicOr(status, kStatusStride);
+    } else {
+        b0 = offs[first];
+        b1 = offs[last];
+        beg = i < npat ? offs[i] : 0;
+        end = i < npat ? offs[i + 1] : 0;
+    }
     const uint64_t len = b1 - b0;
 #ifdef FMX_PHASE_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
@@ -102,7 +115,10 @@ __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pa
 #endif
     // the encoding table (stage_tables, written by every thread) is read below
     __syncthreads();
-    if (len > stage_bytes) return false;
+    if (len > stage_bytes) {
+        if (stride && chk != end) atomicOr(status, kStatusStride);
+        return false;
+    }
     using V4 = uint32_t __attribute__((ext_vector_type(4)));
     const uint64_t a0 = b0 & ~15ull;
     const uint32_t nv = (uint32_t)((b1 - a0 + 15) >> 4);
@@ -128,6 +144,7 @@ __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pa
             }
         }
     }
+    if (stride && chk != end) atomicOr(status, kStatusStride);
     return true;
 }
 
@@ -155,7 +172,8 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
     const uint64_t first = (uint64_t)blockIdx.x * 256u;
     uint64_t beg, end, b0, b1;
-    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, beg, end, b0, b1);
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, flags >> 16, a.status, beg,
+                                       end, b0, b1);
     __syncthreads();
     const uint64_t i = first + threadIdx.x;
     if (i >= npat) return;
@@ -261,7 +279,8 @@ __global__ __launch_bounds__(256, LT ? 4 : 8) void k_locate(const QueryArgs a, c
     const bool rev = B.rev != 0;
     uint64_t beg, end, b0, b1;
     const bool staged =
-        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end, b0, b1);
+        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, B.stride, a.status,
+                       beg, end, b0, b1);
     __syncthreads();
     FMX_STAMP(1, __builtin_amdgcn_s_memrealtime());
     FMX_STAMP(5, g);
@@ -425,7 +444,8 @@ __global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, c
     SearchRec<P> *__restrict__ recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
     uint64_t beg, end, b0, b1;
     const bool staged =
-        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, beg, end, b0, b1);
+        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, B.stride, a.status,
+                       beg, end, b0, b1);
     __syncthreads();
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     uint64_t cnt = 0;
@@ -752,7 +772,7 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
         if (ix->locate_fused) {
             LocateGroup grp{};
             grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles,
-                                   epoch, (flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
+                                   epoch, (flags & FMX_PATTERN_REVERSED) ? 1u : 0u, flags >> 16};
             grp.n = 1;
             if (sb > (uint32_t)kStageBytes)
                 hipLaunchKernelGGL((k_locate<P, N, VB, R, true>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
@@ -764,7 +784,7 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
         }
         LocateGroup grp{};
         grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles, 1u,
-                               (flags & FMX_PATTERN_REVERSED) ? 1u : 0u};
+                               (flags & FMX_PATTERN_REVERSED) ? 1u : 0u, flags >> 16};
         grp.n = 1;
         return launch_split<P, N, VB, R>(ix, grp, (uint32_t)((n + 255) / 256), sb, stream);
     });

@@ -521,3 +521,75 @@ def test_fused_locate_kernel(pkg, O, pb, planes, vb, monkeypatch):
     pats += [rand_pattern(rng, text, 70, 160) for _ in range(300)]  # the long-pattern variant's staging
     for occ in (1, 4 | 8, 63):
         check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, reversed_too=(occ == 63))
+
+
+@pytest.mark.parametrize("m", [1, 3, 20, 150, 300])
+def test_fixed_len_hint(pkg, O, m):
+    """FMX_HINT_FIXED_LEN: the kernels address each pattern at i * m without
+    reading the offsets first.  Grouped batches (forward and reversed, several
+    sizes; m = 300 overflows the 56 KB LDS stage and reads from HBM) and
+    k_count give the oracle's results; offsets that disagree with the hint
+    (a wrong length, a nonzero first offset) are reported as FMX_E_ARG."""
+    import torch
+    rng = np.random.default_rng(100 + m)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=60_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    dev = torch.device("cuda:0")
+    stage_kb = min(56, -(-256 * m // 1024))
+    bats, jobs = [], []
+    for bi, n in enumerate([700, 1, 256, 2049]):
+        rev = bi % 2 == 1
+        starts = rng.integers(0, text.size - m, size=n)
+        pats = [text[s:s + m].tobytes() for s in starts]
+        data, offsets = pkg.pack_patterns(pats)
+        want = orc.locate_batch(data, offsets)
+        q = [p[::-1] for p in pats] if rev else pats
+        data, offsets = pkg.pack_patterns(q)
+        cap = int(want[1].size) + 8
+        b = dict(n=n, want=want, data=torch.from_numpy(data.copy()).to(dev),
+                 off=torch.from_numpy(offsets.view(np.int64).copy()).to(dev),
+                 loff=torch.full((n + 1,), -1, dtype=torch.int64, device=dev),
+                 locs=torch.zeros(cap, dtype=torch.int32, device=dev),
+                 need=torch.zeros(1, dtype=torch.int64, device=dev),
+                 cnt=torch.zeros(n, dtype=torch.int32, device=dev), cnt2=torch.zeros(n, dtype=torch.int32, device=dev))
+        ws = ix.locate_workspace_size(n)
+        b["ws"] = torch.zeros(ws, dtype=torch.uint8, device=dev)
+        jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), n, b["loff"].data_ptr(),
+                                  b["locs"].data_ptr(), cap, b["need"].data_ptr(), b["ws"].data_ptr(), ws,
+                                  d_counts=b["cnt"].data_ptr(), reversed=rev, stage_kb=stage_kb, fixed_len=m))
+        ix.count_batch_async(b["data"].data_ptr(), b["off"].data_ptr(), n, b["cnt2"].data_ptr(),
+                             reversed=rev, stage_kb=stage_kb, fixed_len=m)
+        bats.append(b)
+    ix.sync()
+    ix.locate_group_async(ix.job_queue(jobs))
+    ix.sync()
+    for b in bats:
+        wo, wl = b["want"]
+        assert np.array_equal(b["loff"].cpu().numpy().view(np.uint64), wo)
+        assert np.array_equal(b["locs"].cpu().numpy()[:wl.size].view(np.uint32), wl)
+        assert np.array_equal(b["cnt"].cpu().numpy().view(np.uint32), np.diff(wo).astype(np.uint32))
+        assert np.array_equal(b["cnt2"].cpu().numpy().view(np.uint32), np.diff(wo).astype(np.uint32))
+    # the host API sets the hint itself for equal-length patterns
+    data, offsets = pkg.pack_patterns([text[s:s + m].tobytes() for s in starts])
+    goff, glocs = ix.locate_batch((data, offsets))
+    ooff, olocs = orc.locate_batch(data, offsets)
+    assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    # a hint the offsets contradict
+    b = bats[0]
+    bad = ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), b["n"], b["loff"].data_ptr(),
+                        b["locs"].data_ptr(), int(b["locs"].numel()), b["need"].data_ptr(), b["ws"].data_ptr(),
+                        int(b["ws"].numel()), stage_kb=stage_kb, fixed_len=m + 1)
+    ix.locate_group_async(ix.job_queue([bad]))
+    with pytest.raises(pkg.FmxError):
+        ix.sync()
+    shifted = torch.cat([b["off"][:1] + 1, b["off"][1:]])  # offsets[0] != 0
+    ix.count_batch_async(b["data"].data_ptr(), shifted.data_ptr(), b["n"], b["cnt2"].data_ptr(),
+                         stage_kb=stage_kb, fixed_len=m)
+    with pytest.raises(pkg.FmxError):
+        ix.sync()
+    ix.sync()  # the status was cleared by the failing sync
+    ix.close()
+
