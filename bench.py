@@ -428,6 +428,9 @@ def main():
         "roofline": {
             "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "achieved_basis": "reference algorithm's bytes per pattern (SURVEY.md 8(d)) x patterns per launch / "
+                              "launch time; the derived index structures skip most of those bytes, so frac can "
+                              "exceed 1 - traffic_frac is this kernel's own measured HBM traffic over peak",
             "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pattern": alg_bytes / pats_per_launch,
             "patterns_per_launch": pats_per_launch,
             "avg_launch_ms": kern.get(dominant),

@@ -85,7 +85,7 @@ typedef struct fmx_layout {
                                   breadth-first backward search; replaces the first LF steps.
                                   Indexed by the S symbols that occur in the text: K = the
                                   largest with S^K * 2P bytes <= FMX_DEEP_LUT_MB (environment;
-                                  default 40960, capped at a quarter of free HBM) */
+                                  default 163840, capped at half the free HBM) */
 #define FMX_OPT_FULL_SA 4u     /* the full suffix array (n x P), recovered on the GPU by walking every
                                   row to its sample: a location is one read, no walk            */
 #define FMX_OPT_TEXT 8u        /* the text (n symbol indices), recovered from the full SA; once an

@@ -270,15 +270,19 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         }
     if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
         // the largest K with S^K * 2P <= budget, deeper than the blob's k;
-        // budget: FMX_DEEP_LUT_MB, else 40 GiB capped at a quarter of free HBM
-        uint64_t budget = 40960ull << 20;
+        // budget: FMX_DEEP_LUT_MB, else 160 GiB capped at half the free HBM
+        // (C2: K = 17, 128 GiB, 5 % above K = 16; C5: K = 16, 64 GiB, 9 % above
+        // K = 15; profiles/r1_ab/r1lk*).  The build briefly needs 1/S more.
+        uint64_t budget = 163840ull << 20;
         size_t hfree = 0, htotal = 0;
-        if (hipMemGetInfo(&hfree, &htotal) == hipSuccess) budget = std::min<uint64_t>(budget, hfree / 4);
+        if (hipMemGetInfo(&hfree, &htotal) == hipSuccess) budget = std::min<uint64_t>(budget, hfree / 2);
         if (const char *env = getenv("FMX_DEEP_LUT_MB")) budget = strtoull(env, nullptr, 10) << 20;
         const uint64_t per = 2ull * v.L.pos_bytes;
         uint32_t K = 0;
         uint64_t cnt = 1;
-        while (K < 32 && cnt <= budget / per / S) { cnt *= S; ++K; }
+        // ... and no deeper than the first K with S^K >= 16 n (at most one
+        // text position per 16 entries: deeper buys next to nothing)
+        while (K < 32 && cnt <= budget / per / S && cnt < 16 * v.n) { cnt *= S; ++K; }
         if (K > v.k) {
             q.dlut_sigma = S;
             if (build_deep_lut(ix, K, ix->stream) != hipSuccess) return FMX_E_DEVICE;

@@ -563,10 +563,11 @@ template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *__restrict__ parent, uint64_t np,
                                                     P *__restrict__ child) {
     using O = Occ<P, N, VB, REC>;
-    const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (x >= np) return;
-    const P lo = parent[2 * x], hi = parent[2 * x + 1];
     const P sent = (P)a.sentinel;
+    // grid-stride: a launch covers at most 2^32 - 1 work-items (S^16 parents
+    // for a K = 17 table would not fit one thread each)
+    for (uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x; x < np; x += (uint64_t)gridDim.x * 256u) {
+    const P lo = parent[2 * x], hi = parent[2 * x + 1];
     for (uint32_t d = 0; d < a.dlut_sigma; ++d) {
         const uint32_t c = a.dlut_sym[d];
         P clo = 0, chi = 0;
@@ -578,6 +579,7 @@ __global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *
         P *dst = child + 2 * ((uint64_t)d * np + x);
         dst[0] = clo;
         dst[1] = chi;
+    }
     }
 }
 
@@ -720,6 +722,11 @@ static hipError_t dispatch(const fmx_index *ix, F &&f) {
 }
 
 static inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
+// k_dlut_level: one thread per parent up to 2^24 workgroups, then grid-stride
+static inline unsigned grid_dlut(uint64_t np) {
+    const uint64_t g = (np + 255) / 256;
+    return (unsigned)(g < (1ull << 24) ? (g ? g : 1) : (1ull << 24) - 1);
+}
 
 // look-back tiles needed for n patterns (one per 256-pattern workgroup)
 uint64_t locate_tiles_cap(uint64_t n) { return (n + 255) / 256 > 0 ? (n + 255) / 256 : 1; }
@@ -838,7 +845,7 @@ hipError_t build_deep_lut(fmx_index *ix, uint32_t K, hipStream_t stream) {
         hipLaunchKernelGGL((k_dlut_root<P>), dim3(1), dim3(64), 0, stream, qa, (P *)buf(1));
         uint64_t np = sigma;
         for (uint32_t j = 1; j < K; ++j) {
-            hipLaunchKernelGGL((k_dlut_level<P, N, VB, R>), dim3(grid_for(np)), dim3(256), 0, stream, qa,
+            hipLaunchKernelGGL((k_dlut_level<P, N, VB, R>), dim3(grid_dlut(np)), dim3(256), 0, stream, qa,
                                (const P *)buf(j), np, (P *)buf(j + 1));
             np *= sigma;
         }
