@@ -259,6 +259,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     }
     ix->options = ix->occ_mode;
     if (const char *env = getenv("FMX_LOCATE_FUSED")) ix->locate_fused = atoi(env) != 0;
+    if (const char *env = getenv("FMX_TILE_PAIRS")) ix->tile_pairs = atoi(env) != 0;
     // deep-table digits: the symbols that occur in the text (a pattern holding
     // any other symbol is left to the blob's seed and the LF loop)
     uint32_t S = 0;

@@ -422,6 +422,31 @@ FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w
     return 0;
 }
 
+// The deep k-mer table's index for the last K symbols of the pattern, or
+// false when the table does not apply (no table, m < K, a symbol that does
+// not occur in the text or is >= sigma: the blob's seed and the LF loop then
+// empty the interval — or reject the symbol — exactly there).
+template <typename P>
+FMX_HD bool dlut_code(const QueryArgs &a, const Tables<P> &s, const PatView &pv, uint64_t &code) {
+    code = 0;
+    if (a.dlut == nullptr || pv.m == 0 || pv.m < a.dlut_k) return false;
+    const uint32_t K = a.dlut_k, S = a.dlut_sigma, sigma = a.sigma;
+    const uint64_t m = pv.m;
+    uint32_t miss = 0;
+#pragma unroll 4
+    for (uint32_t j = 0; j < K; ++j) {
+        const uint32_t c = pv.at(m - K + j);
+        const uint32_t d = c < sigma ? s.dig[c] : kNoDigit;
+        miss |= d == kNoDigit;
+        code = code * S + d;
+    }
+    return !miss;
+}
+
+template <typename P, int N, int VB, int REC, bool LT = false>
+FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatView &pv, bool have, P w0, P w1,
+                              P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode);
+
 // k-mer seed + LF loop: FmIndex::get_pos_range (with_slice.rs:21-33).
 // Returns status bits (0 = ok).  The result is the interval [lo, hi) with
 // mode kHitRows, or (derived structures) an interval finished early: a
@@ -430,6 +455,23 @@ FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w
 template <typename P, int N, int VB, int REC, bool LT = false>
 FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv, P &lo, P &hi, P &rloc,
                        uint64_t &mask, uint32_t &mode) {
+    uint64_t code;
+    const bool have = dlut_code<P>(a, s, pv, code);
+    P w0 = 0, w1 = 0;
+    if (have) {
+        const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
+        w0 = dl[0];
+        w1 = dl[1];
+    }
+    return search_seeded<P, N, VB, REC, LT>(a, s, pv, have, w0, w1, lo, hi, rloc, mask, mode);
+}
+
+// search() after the deep-table read: `have` = the entry {w0, w1} of the
+// pattern's last K symbols (the interval K-k more LF steps from the blob's
+// seed reach, or a single-row entry) was read.
+template <typename P, int N, int VB, int REC, bool LT>
+FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatView &pv, bool have, P w0, P w1,
+                              P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode) {
     using O = Occ<P, N, VB, REC>;
     const uint32_t sigma = a.sigma, k = a.k;
     const uint64_t m = pv.m;
@@ -442,31 +484,12 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
     uint64_t idx = 0;
     uint32_t bad = 0;
     bool seeded = false;
-    if (a.dlut != nullptr && m >= a.dlut_k) {
-        // deep k-mer table over the symbols that occur in the text: the SA
-        // interval of the last K symbols in one read (the interval K-k more LF
-        // steps from the blob's seed reach).  A symbol that does not occur (or
-        // is >= sigma) leaves the pattern to the blob's seed and the LF loop,
-        // which empty the interval — or reject the symbol — exactly there.
-        const uint32_t K = a.dlut_k, S = a.dlut_sigma;
-        uint64_t code = 0;
-        uint32_t miss = 0;
-#pragma unroll 4
-        for (uint32_t j = 0; j < K; ++j) {
-            const uint32_t c = pv.at(m - K + j);
-            const uint32_t d = c < sigma ? s.dig[c] : kNoDigit;
-            miss |= d == kNoDigit;
-            code = code * S + d;
-        }
-        if (!miss) {
-            const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
-            const P w0 = dl[0], w1 = dl[1];
-            idx = m - K;
-            if (a.dlut_rows && (w0 & row_flag<P>())) return one_row<P, LT>(a, pv, idx, w0, w1, lo, hi, rloc, mode);
-            lo = w0;
-            hi = w1;
-            seeded = true;
-        }
+    if (have) {
+        idx = m - a.dlut_k;
+        if (a.dlut_rows && (w0 & row_flag<P>())) return one_row<P, LT>(a, pv, idx, w0, w1, lo, hi, rloc, mode);
+        lo = w0;
+        hi = w1;
+        seeded = true;
     }
     if (!seeded) {
         // seed: count_array.rs:203-233

@@ -122,6 +122,7 @@ struct fmx_index {
     uint64_t safull_bytes = 0;
     uint8_t *d_text = nullptr;
     uint32_t options = 0;
+    bool tile_pairs = false;  // FMX_TILE_PAIRS=1: k_search2 (two tiles per workgroup, entry reads paired)
     bool locate_fused = false;  // FMX_LOCATE_FUSED=1: the single-kernel k_locate (look-back) instead of
                                 // k_search + k_scan + k_emit
     fmx::QueryArgs qa{};

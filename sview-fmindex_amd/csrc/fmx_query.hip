@@ -84,39 +84,52 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total,
 // aligned vectors, up to four per thread in flight (an aligned vector holding
 // at least one byte of the batch never leaves the batch's page).  Returns
 // false if the tile does not fit; the patterns are then read from HBM.
-template <typename P>
-__device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
-                                               const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
-                                               uint32_t stage_bytes, uint32_t stride, uint32_t *status,
-                                               uint64_t &beg, uint64_t &end, uint64_t &b0, uint64_t &b1) {
-    const uint64_t last = first + 256 < npat ? first + 256 : npat;
-    const uint64_t i = first + threadIdx.x;
-    uint64_t chk = 0;
+// NP patterns per thread (a pair of tiles: NP = 2): thread t stages and
+// later searches patterns first + t, first + 256 + t, ... of one span.
+template <typename P, int NP>
+__device__ __forceinline__ bool stage_span(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
+                                           const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
+                                           uint32_t stage_bytes, uint32_t stride, uint32_t *status,
+                                           uint64_t *beg, uint64_t *end, uint64_t &b0, uint64_t &b1) {
+    const uint64_t last = first + 256 * NP < npat ? first + 256 * NP : npat;
+    uint64_t chk[NP];
     if (stride) {
         // FMX_HINT_FIXED_LEN: offs[i] == i * stride, so the byte loads need
-        // not wait for the offsets; each thread's own end offset is loaded
+        // not wait for the offsets; each thread's own end offsets are loaded
         // alongside them and checked once they have arrived.
         b0 = first * stride;
         b1 = last * stride;
-        beg = i < npat ? i * stride : 0;
-        end = i < npat ? beg + stride : 0;
-        chk = i < npat ? offs[i + 1] : 0;
-        if (i == 0 && offs[0] != 0) atomicOr(status, kStatusStride);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const uint64_t i = first + 256 * q + threadIdx.x;
+            beg[q] = i < npat ? i * stride : 0;
+            end[q] = i < npat ? beg[q] + stride : 0;
+            chk[q] = i < npat ? offs[i + 1] : 0;
+        }
+        if (first == 0 && threadIdx.x == 0 && offs[0] != 0) atomicOr(status, kStatusStride);
     } else {
         b0 = offs[first];
         b1 = offs[last];
-        beg = i < npat ? offs[i] : 0;
-        end = i < npat ? offs[i + 1] : 0;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const uint64_t i = first + 256 * q + threadIdx.x;
+            beg[q] = i < npat ? offs[i] : 0;
+            end[q] = i < npat ? offs[i + 1] : 0;
+            chk[q] = end[q];
+        }
     }
     const uint64_t len = b1 - b0;
 #ifdef FMX_PHASE_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
-    FMX_STAMP(7, __builtin_amdgcn_s_memrealtime() + (beg & 0) + (end & 0) + (len & 0));
+    FMX_STAMP(7, __builtin_amdgcn_s_memrealtime() + (beg[0] & 0) + (end[0] & 0) + (len & 0));
 #endif
+    uint32_t bad_stride = 0;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) bad_stride |= chk[q] != end[q];
     // the encoding table (stage_tables, written by every thread) is read below
     __syncthreads();
     if (len > stage_bytes) {
-        if (stride && chk != end) atomicOr(status, kStatusStride);
+        if (bad_stride) atomicOr(status, kStatusStride);
         return false;
     }
     using V4 = uint32_t __attribute__((ext_vector_type(4)));
@@ -144,8 +157,17 @@ __device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pa
             }
         }
     }
-    if (stride && chk != end) atomicOr(status, kStatusStride);
+    if (bad_stride) atomicOr(status, kStatusStride);
     return true;
+}
+
+template <typename P>
+__device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
+                                               const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
+                                               uint32_t stage_bytes, uint32_t stride, uint32_t *status,
+                                               uint64_t &beg, uint64_t &end, uint64_t &b0, uint64_t &b1) {
+    return stage_span<P, 1>(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, stride, status, &beg, &end, b0,
+                            b1);
 }
 
 template <typename P>
@@ -417,29 +439,25 @@ __device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &
 // workspace = [256 B][tile counts: G][tile offsets: G][search records: n].
 
 // This workgroup's batch of a grouped launch (workgroup-uniform).
-__device__ __forceinline__ uint32_t group_batch(const LocateGroup &grp) {
+__device__ __forceinline__ uint32_t group_batch(const LocateGroup &grp, uint32_t vt) {
     uint32_t jb = 0;
 #pragma unroll
     for (uint32_t t = 1; t < kMaxGroup; ++t)
-        if (t < grp.n && blockIdx.x >= grp.tile_begin[t]) jb = t;
+        if (t < grp.n && vt >= grp.tile_begin[t]) jb = t;
     return jb;
 }
 
 // 1. Search every pattern; its result record, its count; the tile's count.
 template <typename P, int N, int VB, int REC, bool LT>
-__global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
-                                                             uint32_t stage_bytes) {
-    __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
-    __shared__ uint64_t s_scan[4];
-    stage_tables(a, s);
-    const uint32_t jb = group_batch(grp);
+__device__ __forceinline__ void search_tile(const QueryArgs &a, const LocateGroup &grp, const Tables<P> &s,
+                                            uint8_t *s_pat, uint64_t *s_scan, uint32_t stage_bytes, uint32_t vt) {
+    const uint32_t jb = group_batch(grp, vt);
     const LocateBatch &B = grp.b[jb];
     const uint8_t *__restrict__ bytes = B.bytes;
     const uint64_t *__restrict__ offs = B.offs;
     const uint64_t npat = B.npat;
     const bool rev = B.rev != 0;
-    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
+    const uint32_t g = vt - grp.tile_begin[jb];
     const uint64_t G = (npat + 255) / 256;
     SearchRec<P> *__restrict__ recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
     uint64_t beg, end, b0, b1;
@@ -461,8 +479,90 @@ __global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, c
         recs[i] = pack_rec<P>(lo, hi, rloc, mask, mode);
     }
     uint64_t agg;
-    block_excl_scan(cnt, &agg, s_scan);
+    block_excl_scan(cnt, &agg, s_scan);  // (its barriers end every read of s_pat)
     if (threadIdx.x == 0) B.tiles[g] = agg;
+}
+
+template <typename P, int N, int VB, int REC, bool LT>
+__global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
+                                                             uint32_t stage_bytes) {
+    __shared__ Tables<P> s;
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
+    __shared__ uint64_t s_scan[4];
+    stage_tables(a, s);
+    search_tile<P, N, VB, REC, LT>(a, grp, s, s_pat, s_scan, stage_bytes, blockIdx.x);
+}
+
+// k_search over a pair of tiles per workgroup (FMX_TILE_PAIRS=1): each lane
+// owns one pattern of each tile, the pair is staged as one span (one round
+// trip for the offsets, one for the bytes) and both patterns' deep-table
+// entries are read before either is used — twice the dependent requests in
+// flight per wave slot.  A pair split across two batches of a group (or a
+// lone last tile) runs tile by tile.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256, 8) void k_search2(const QueryArgs a, const LocateGroup grp,
+                                                    uint32_t stage_bytes, uint32_t ntiles) {
+    __shared__ Tables<P> s;
+    extern __shared__ uint8_t s_pat[];  // 2 * stage_bytes, dynamic
+    __shared__ uint64_t s_scan[4];
+    stage_tables(a, s);
+    const uint32_t vt0 = 2u * blockIdx.x, vt1 = vt0 + 1u;
+    const uint32_t jb = group_batch(grp, vt0);
+    if (vt1 >= ntiles || group_batch(grp, vt1) != jb) {  // workgroup-uniform
+        search_tile<P, N, VB, REC, false>(a, grp, s, s_pat, s_scan, stage_bytes, vt0);
+        if (vt1 < ntiles) search_tile<P, N, VB, REC, false>(a, grp, s, s_pat, s_scan, stage_bytes, vt1);
+        return;
+    }
+    const LocateBatch &B = grp.b[jb];
+    const uint8_t *__restrict__ bytes = B.bytes;
+    const uint64_t npat = B.npat;
+    const bool rev = B.rev != 0;
+    const uint32_t g = vt0 - grp.tile_begin[jb];
+    const uint64_t G = (npat + 255) / 256;
+    SearchRec<P> *__restrict__ recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
+    uint64_t beg[2], end[2], b0, b1;
+    const bool staged = stage_span<P, 2>(s, s_pat, bytes, B.offs, npat, (uint64_t)g * 256u, rev, 2 * stage_bytes,
+                                         B.stride, a.status, beg, end, b0, b1);
+    __syncthreads();
+    const uint64_t i0 = (uint64_t)g * 256u + threadIdx.x, i1 = i0 + 256u;
+    const bool v0 = i0 < npat, v1 = i1 < npat;
+    const PatView pv0 = pattern_view(s, s_pat, staged, bytes, beg[0], end[0], b0, b1, rev);
+    const PatView pv1 = pattern_view(s, s_pat, staged, bytes, beg[1], end[1], b0, b1, rev);
+    uint64_t c0 = 0, c1 = 0;
+    const bool h0 = v0 && dlut_code<P>(a, s, pv0, c0);
+    const bool h1 = v1 && dlut_code<P>(a, s, pv1, c1);
+    const P *dl = reinterpret_cast<const P *>(a.dlut);
+    P w00 = 0, w01 = 0, w10 = 0, w11 = 0;
+    if (h0) { w00 = dl[2 * c0]; w01 = dl[2 * c0 + 1]; }
+    if (h1) { w10 = dl[2 * c1]; w11 = dl[2 * c1 + 1]; }
+    uint64_t cnt0 = 0, cnt1 = 0;
+    if (v0) {
+        P lo, hi, rloc;
+        uint64_t mask;
+        uint32_t mode;
+        const uint32_t bad = search_seeded<P, N, VB, REC, false>(a, s, pv0, h0, w00, w01, lo, hi, rloc, mask, mode);
+        if (bad) atomicOr(a.status, bad);
+        cnt0 = (uint64_t)(hi - lo);
+        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i0] = hi - lo;
+        recs[i0] = pack_rec<P>(lo, hi, rloc, mask, mode);
+    }
+    if (v1) {
+        P lo, hi, rloc;
+        uint64_t mask;
+        uint32_t mode;
+        const uint32_t bad = search_seeded<P, N, VB, REC, false>(a, s, pv1, h1, w10, w11, lo, hi, rloc, mask, mode);
+        if (bad) atomicOr(a.status, bad);
+        cnt1 = (uint64_t)(hi - lo);
+        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i1] = hi - lo;
+        recs[i1] = pack_rec<P>(lo, hi, rloc, mask, mode);
+    }
+    uint64_t agg0, agg1;
+    block_excl_scan(cnt0, &agg0, s_scan);
+    block_excl_scan(cnt1, &agg1, s_scan);
+    if (threadIdx.x == 0) {
+        B.tiles[g] = agg0;
+        B.tiles[g + 1] = agg1;
+    }
 }
 
 // 2. One workgroup per batch: exclusive scan of its tile counts into tile
@@ -511,7 +611,7 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
     __shared__ P sC[kMaxSigma + 1];
     __shared__ uint64_t s_scan[4];
     if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
-    const uint32_t jb = group_batch(grp);
+    const uint32_t jb = group_batch(grp, blockIdx.x);
     const LocateBatch &B = grp.b[jb];
     const uint64_t npat = B.npat, G = (npat + 255) / 256;
     const uint64_t g = blockIdx.x - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
@@ -758,6 +858,9 @@ static hipError_t launch_split(const fmx_index *ix, const LocateGroup &grp, uint
                                hipStream_t stream) {
     if (sb > (uint32_t)kStageBytes)
         hipLaunchKernelGGL((k_search<P, N, VB, R, true>), dim3(tiles), dim3(256), sb, stream, ix->qa, grp, sb);
+    else if (ix->tile_pairs && ix->qa.dlut != nullptr)
+        hipLaunchKernelGGL((k_search2<P, N, VB, R>), dim3((tiles + 1) / 2), dim3(256), 2 * sb, stream, ix->qa, grp,
+                           sb, tiles);
     else
         hipLaunchKernelGGL((k_search<P, N, VB, R, false>), dim3(tiles), dim3(256), sb, stream, ix->qa, grp, sb);
     uint32_t fold = 1;
