@@ -498,9 +498,10 @@ __global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, c
 // trip for the offsets, one for the bytes) and both patterns' deep-table
 // entries are read before either is used — twice the dependent requests in
 // flight per wave slot.  A pair split across two batches of a group (or a
-// lone last tile) runs tile by tile.
+// lone last tile) runs tile by tile.  6 waves/SIMD (80 VGPRs): at 8 the
+// pair spilled 55 VGPRs.
 template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256, 8) void k_search2(const QueryArgs a, const LocateGroup grp,
+__global__ __launch_bounds__(256, 6) void k_search2(const QueryArgs a, const LocateGroup grp,
                                                     uint32_t stage_bytes, uint32_t ntiles) {
     __shared__ Tables<P> s;
     extern __shared__ uint8_t s_pat[];  // 2 * stage_bytes, dynamic
