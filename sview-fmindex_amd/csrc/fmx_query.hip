@@ -136,6 +136,9 @@ __device__ __forceinline__ bool stage_span(const Tables<P> &s, uint8_t *s_pat, c
     const uint64_t a0 = b0 & ~15ull;
     const uint32_t nv = (uint32_t)((b1 - a0 + 15) >> 4);
     const V4 *src = reinterpret_cast<const V4 *>(bytes + a0);
+    // 32-bit positions within the span (len <= stage_bytes): byte w of
+    // vector v is span byte 16 v + w - lead, kept if below len (unsigned)
+    const uint32_t lead = (uint32_t)(b0 - a0), len32 = (uint32_t)len;
     for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 256) {
         V4 x[4];
 #pragma unroll
@@ -147,13 +150,12 @@ __device__ __forceinline__ bool stage_span(const Tables<P> &s, uint8_t *s_pat, c
         for (uint32_t u = 0; u < 4; ++u) {
             const uint32_t v = v0 + u * 256 + threadIdx.x;
             if (v >= nv) continue;
+            const uint32_t base = 16u * v - lead;
 #pragma unroll
             for (uint32_t w = 0; w < 16; ++w) {
-                const uint64_t pos = a0 + 16ull * v + w;
-                if (pos >= b0 && pos < b1) {
-                    const uint64_t x0 = pos - b0;
-                    s_pat[rev ? len - 1 - x0 : x0] = s.enc[(x[u][w >> 2] >> (8 * (w & 3))) & 0xffu];
-                }
+                const uint32_t x0 = base + w;
+                if (x0 < len32)
+                    s_pat[rev ? len32 - 1u - x0 : x0] = s.enc[(x[u][w >> 2] >> (8 * (w & 3))) & 0xffu];
             }
         }
     }
