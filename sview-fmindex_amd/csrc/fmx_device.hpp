@@ -433,6 +433,17 @@ FMX_HD bool dlut_code(const QueryArgs &a, const Tables<P> &s, const PatView &pv,
     const uint32_t K = a.dlut_k, S = a.dlut_sigma, sigma = a.sigma;
     const uint64_t m = pv.m;
     uint32_t miss = 0;
+    if (pv.sym != nullptr) {  // staged (the common case): no per-symbol source test
+        const uint8_t *q = pv.sym + (m - K);
+#pragma unroll 4
+        for (uint32_t j = 0; j < K; ++j) {
+            const uint32_t c = q[j];
+            const uint32_t d = c < sigma ? s.dig[c] : kNoDigit;
+            miss |= d == kNoDigit;
+            code = code * S + d;
+        }
+        return !miss;
+    }
 #pragma unroll 4
     for (uint32_t j = 0; j < K; ++j) {
         const uint32_t c = pv.at(m - K + j);
