@@ -403,10 +403,19 @@ FMX_HD uint32_t one_row(const QueryArgs &a, const PatView &pv, uint64_t idx, P w
     const uint64_t x = (uint64_t)w1;
     const uint64_t L = idx < Ld ? idx : Ld;
     uint64_t pc = 0;
-    for (uint64_t j = 0; j < L; ++j) {
-        const uint32_t c = pv.at(idx - 1 - j);
-        const uint64_t d = c < a.sigma ? c + 1 : a.sigma + 1;  // sigma + 1: never a stored digit
-        pc |= d << (bps * j);
+    if (pv.sym != nullptr) {  // staged: no per-symbol source test
+        const uint8_t *q = pv.sym + idx - 1;
+        for (uint32_t j = 0; j < (uint32_t)L; ++j) {
+            const uint32_t c = q[-(int32_t)j];
+            const uint64_t d = c < a.sigma ? c + 1 : a.sigma + 1;  // sigma + 1: never a stored digit
+            pc |= d << (bps * j);
+        }
+    } else {
+        for (uint64_t j = 0; j < L; ++j) {
+            const uint32_t c = pv.at(idx - 1 - j);
+            const uint64_t d = c < a.sigma ? c + 1 : a.sigma + 1;
+            pc |= d << (bps * j);
+        }
     }
     const uint64_t keep = L * bps >= 64 ? ~0ull : (1ull << (L * bps)) - 1;
     const uint64_t diff = (pc ^ (uint64_t)(w0 & (P)~row_flag<P>())) & keep;
