@@ -69,34 +69,6 @@ CONFIGS = {
 }
 
 
-def phase_stamps(pkg, ix, step, B, out_path):
-    """Diagnostic (FMX_LIB=.../libfmx_stamps.so): per-wave phase timestamps of
-    one k_locate launch, summarised as percentiles (10 ns ticks -> us)."""
-    import ctypes
-    import torch
-    L = pkg._native.lib()
-    torch.cuda.synchronize()
-    step()
-    torch.cuda.synchronize()
-    waves = (B + 255) // 256 * 4
-    buf = np.zeros(waves * 8, np.uint64)
-    L.fmx_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    assert L.fmx_debug_stamps(buf.ctypes.data, buf.size) == 0
-    t = buf.reshape(waves, 8).astype(np.float64)
-    live = np.arange(waves) * 64 < B
-    t = t[live]
-    t0 = t[:, 0].min()
-    rel = (t - t0) / 100.0  # us
-    pct = lambda x: {q: round(float(np.percentile(x, q)), 2) for q in (0, 10, 50, 90, 100)}
-    res = {"waves": int(live.sum()), "entry": pct(rel[:, 0]), "tile_id": pct(rel[:, 6]), "offs_loaded": pct(rel[:, 7]),
-           "staged": pct(rel[:, 1]), "searched": pct(rel[:, 2]),
-           "offsets": pct(rel[:, 3]), "done": pct(rel[:, 4]),
-           "stage_us": pct(rel[:, 1] - rel[:, 0]), "search_us": pct(rel[:, 2] - rel[:, 1]),
-           "lookback_us": pct(rel[:, 3] - rel[:, 2]), "locate_us": pct(rel[:, 4] - rel[:, 3])}
-    json.dump(res, open(out_path, "w"), indent=1)
-    log("[stamps] " + json.dumps(res))
-
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,9 +300,6 @@ def main():
 
     for bt in batches:
         ix.sync(bt["stream"].cuda_stream)
-    if os.environ.get("FMX_STAMPS_OUT"):
-        phase_stamps(pkg, ix, step, B, os.environ["FMX_STAMPS_OUT"])
-        torch.cuda.synchronize()
 
     # ---- result concatenation across ranks (RCCL all-gathers, untimed) -----
     gather_ms = None
@@ -369,8 +338,6 @@ def main():
     achieved = alg_bytes / (kern[dominant] * 1e-3) / 1e9
     traffic, traffic_src = None, None
     key = f"{args.config}:{n}:{B}:{m}:{info['options']}:{info['deep_lut_k']}" + (f":g{GR}" if native and GR > 1 else "")
-    if os.environ.get("FMX_LOCATE_FUSED", "0") not in ("", "0"):
-        key += ":fused"
     if os.path.exists(args.traffic_json):
         try:
             pm = json.load(open(args.traffic_json))

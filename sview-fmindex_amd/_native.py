@@ -116,7 +116,7 @@ def lib():
                 import torch  # noqa: F401
             except ImportError:
                 pass
-        L = C.CDLL(os.environ.get("FMX_LIB", LIB_PATH))  # FMX_LIB: a diagnostic build (csrc `make stamps`)
+        L = C.CDLL(os.environ.get("FMX_LIB", LIB_PATH))  # FMX_LIB: another build of the engine
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)
             f.restype = res

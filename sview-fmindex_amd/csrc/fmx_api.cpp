@@ -193,7 +193,11 @@ static Timer &timer(fmx_index *ix, const char *name) {
 // Bracket one launch with events on its stream when timing is on.
 template <class F>
 static hipError_t timed(fmx_index *ix, const char *name, hipStream_t s, uint64_t units, F &&launch) {
-    if (!ix->timing || (ix->timing_seq++ % ix->timing_every) != 0) return launch();
+    std::unique_lock<std::mutex> g(ix->timing_mu);
+    if (!ix->timing || (ix->timing_seq++ % ix->timing_every) != 0) {
+        g.unlock();
+        return launch();
+    }
     hipEvent_t a = take_event(ix), b = take_event(ix);
     if (!a || !b) return hipErrorOutOfMemory;
     hipEventRecord(a, s);
@@ -206,6 +210,33 @@ static hipError_t timed(fmx_index *ix, const char *name, hipStream_t s, uint64_t
 }
 
 static fmx_status dev_err(hipError_t e) { return e == hipSuccess ? FMX_OK : FMX_E_DEVICE; }
+
+// Makes the index's device current for one entry point and restores the
+// caller's current device on every return path.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
+// The status word of `s`: every stream an index launches on gets a device
+// word of its own, so fmx_sync(s) reads and clears only what that stream's
+// launches latched (stream-ordered), never another stream's.
+static uint32_t *status_slot(fmx_index *ix, hipStream_t s) {
+    std::lock_guard<std::mutex> g(ix->status_mu);
+    auto it = ix->status_of.find((const void *)s);
+    if (it != ix->status_of.end()) return it->second;
+    if (ix->status_used >= kStatusSlots) return nullptr;
+    uint32_t *w = ix->d_status + ix->status_used++;
+    ix->status_of.emplace((const void *)s, w);
+    return w;
+}
 
 static fmx_status ensure_scratch(fmx_index *ix, uint64_t bytes) {
     if (ix->scratch_bytes >= bytes) return FMX_OK;
@@ -240,9 +271,14 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     memcpy(q.mult, v.mult, sizeof(q.mult));
     memcpy(q.enc, v.enc, 256);
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
-    if (hipMalloc(&ix->d_status, 64) != hipSuccess) return FMX_E_DEVICE;
-    if (hipMemset(ix->d_status, 0, 64) != hipSuccess) return FMX_E_DEVICE;
-    q.status = ix->d_status;
+    if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMemset(ix->d_status, 0, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
+    q.status = status_slot(ix, ix->stream);
+    // the k-mer count table (W^k entries of P) goes to LDS when it is small
+    {
+        const uint64_t ktb = v.kmer_len * v.L.pos_bytes;
+        q.kt_lds_bytes = ktb <= kKmerLdsMax && ktb % 4 == 0 ? (uint32_t)ktb : 0u;
+    }
     ix->occ_mode = FMX_OCC_BLOB;
     if (options & FMX_OCC_INTERLEAVED) {
         const uint32_t rec = interleaved_record_bytes(v);
@@ -258,8 +294,6 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         }
     }
     ix->options = ix->occ_mode;
-    if (const char *env = getenv("FMX_LOCATE_FUSED")) ix->locate_fused = atoi(env) != 0;
-    if (const char *env = getenv("FMX_TILE_PAIRS")) ix->tile_pairs = atoi(env) != 0;
     // deep-table digits: the symbols that occur in the text (a pattern holding
     // any other symbol is left to the blob's seed and the LF loop)
     uint32_t S = 0;
@@ -337,14 +371,15 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
 }
 
 static fmx_status read_status(fmx_index *ix, hipStream_t s) {
+    uint32_t *w = status_slot(ix, s);
+    if (!w) return FMX_E_DEVICE;
     uint32_t st = 0;
-    if (hipMemcpyAsync(&st, ix->d_status, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMemcpyAsync(&st, w, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
     if (hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
     if (st) {
-        hipMemsetAsync(ix->d_status, 0, 4, s);
-        hipStreamSynchronize(s);
+        // ordered on s after every launch that could have set it: nothing is lost
+        if (hipMemsetAsync(w, 0, 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
     }
-    if (st & kStatusHang) return FMX_E_DEVICE;
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
     if (st & kStatusStride) return FMX_E_ARG;
@@ -398,7 +433,8 @@ fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, i
     };
     fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
     if (st) return st;
-    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    DeviceGuard dg(device);
+    if (!dg.ok) return FMX_E_DEVICE;
     fmx_index *ix = new (std::nothrow) fmx_index();
     if (!ix) return FMX_E_DEVICE;
     ix->bv = bv;
@@ -423,7 +459,8 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
     *out = nullptr;
     if (!layout_valid(layout)) return FMX_E_LAYOUT;
     if (((uintptr_t)d_blob) % align_of(layout) != 0) return FMX_E_ALIGN;
-    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    DeviceGuard dg(device);
+    if (!dg.ok) return FMX_E_DEVICE;
     BlobView bv;
     BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
         if (off + len > blob_len) return false;
@@ -503,7 +540,8 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
     };
     fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
     if (st) { close(fd); return st; }
-    if (hipSetDevice(device) != hipSuccess) { close(fd); return FMX_E_DEVICE; }
+    DeviceGuard dg(device);
+    if (!dg.ok) { close(fd); return FMX_E_DEVICE; }
     fmx_index *ix = new (std::nothrow) fmx_index();
     if (!ix) { close(fd); return FMX_E_DEVICE; }
     ix->bv = bv;
@@ -527,7 +565,7 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
 
 void fmx_free(fmx_index *ix) {
     if (!ix) return;
-    hipSetDevice(ix->device);
+    DeviceGuard dg(ix->device);
     if (ix->stream) hipStreamSynchronize(ix->stream);
     for (auto &t : ix->timers)
         for (auto &p : t.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
@@ -576,13 +614,16 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
                                  uint32_t flags, void *d_counts, void *stream) {
     if (!ix || (n && (!d_bytes || !d_offsets || !d_counts))) return FMX_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    uint32_t *status = status_slot(ix, s);
+    if (!status) return FMX_E_DEVICE;
+    DeviceGuard dg(ix->device);
     return dev_err(timed(ix, "count", s, n, [&] {
-        return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, s);
+        return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, status, s);
     }));
 }
 
-// Locate workspace: [ctl: 2 x u32, padded to 256 B][tiles: 2 x tiles_cap x u64]
-// [search records: n x locate_rec_bytes(P)].
+// Locate workspace: [256 B reserved][tile counts: G][tile offsets: G]
+// [search records: n x locate_rec_bytes(P)], G = ceil(n / 256).
 static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) {
     return 256 + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes);
 }
@@ -593,45 +634,26 @@ fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes)
     return FMX_OK;
 }
 
-// The next look-back epoch of a workspace (k_locate); after kLocateEpochs
-// launches, the tiles any of them published are zeroed (stream-ordered before
-// this launch) and the epochs start again.
-static fmx_status next_epoch(fmx_index *ix, void *d_ws, uint64_t tiles, hipStream_t s, uint32_t *epoch) {
-    uint64_t clear_tiles = 0;
-    {
-        std::lock_guard<std::mutex> g(ix->ws_mu);
-        fmx_index::WsState &w = ix->ws_state[d_ws];
-        if (w.epoch >= kLocateEpochs) {
-            clear_tiles = w.hi_tiles;
-            w.epoch = 0;
-        }
-        *epoch = ++w.epoch;
-        w.hi_tiles = std::max(w.hi_tiles, tiles);
-    }
-    if (clear_tiles && hipMemsetAsync((uint8_t *)d_ws + 256, 0, clear_tiles * 8, s) != hipSuccess)
-        return FMX_E_DEVICE;
-    return FMX_OK;
-}
-
 fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                                   uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs,
                                   uint64_t cap, uint64_t *d_needed, void *d_ws, uint64_t ws_bytes, void *stream) {
     if (!ix || !d_loc_offsets || !d_needed || (n && (!d_bytes || !d_offsets)) || (cap && !d_locs)) return FMX_E_ARG;
     if (!d_ws || ws_bytes < 256 + 16) return FMX_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    DeviceGuard dg(ix->device);
     if (n == 0) {
         hipError_t e = hipMemsetAsync(d_loc_offsets, 0, 8, s);
         if (e == hipSuccess) e = hipMemsetAsync(d_needed, 0, 8, s);
         return dev_err(e);
     }
     if (ws_bytes < ws_bytes_for(ix, n)) return FMX_E_ARG;
+    uint32_t *status = status_slot(ix, s);
+    if (!status) return FMX_E_DEVICE;
     uint8_t *ws = (uint8_t *)d_ws;
     const uint64_t G = locate_tiles_cap(n);
-    uint32_t epoch = 0;
-    if (ix->locate_fused && next_epoch(ix, d_ws, G, s, &epoch) != FMX_OK) return FMX_E_DEVICE;
     return dev_err(timed(ix, "locate", s, n, [&] {
         return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
-                             (uint32_t *)ws, (uint64_t *)(ws + 256), G, epoch, s);
+                             (uint64_t *)(ws + 256), G, status, s);
     }));
 }
 
@@ -657,8 +679,11 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
             j.reserved != 0)
             return FMX_E_ARG;
         for (uint64_t k = 0; k < i; ++k)
-            if (jobs[k].d_workspace == j.d_workspace) return FMX_E_ARG;  // one look-back per workspace
+            if (jobs[k].d_workspace == j.d_workspace) return FMX_E_ARG;  // the batches run concurrently
     }
+    uint32_t *status = status_slot(ix, s);
+    if (!status) return FMX_E_DEVICE;
+    DeviceGuard dg(ix->device);
     // up to kMaxGroup non-empty batches per launch; empty ones get their
     // zero offset and total directly
     uint64_t i = 0;
@@ -675,12 +700,10 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
                 continue;
             }
             const uint64_t G = locate_tiles_cap(j.n_patterns);
-            uint32_t epoch = 1;  // (the split kernels need none)
-            if (ix->locate_fused && next_epoch(ix, j.d_workspace, G, s, &epoch) != FMX_OK) return FMX_E_DEVICE;
             grp.tile_begin[grp.n] = tiles;
             grp.b[grp.n++] = LocateBatch{j.d_bytes, j.d_offsets, j.n_patterns, j.d_counts, j.d_loc_offsets,
                                          j.d_locs, j.cap, j.d_needed, (uint64_t *)((uint8_t *)j.d_workspace + 256),
-                                         epoch, (j.flags & FMX_PATTERN_REVERSED) ? 1u : 0u, j.flags >> 16};
+                                         (j.flags & FMX_PATTERN_REVERSED) ? 1u : 0u, j.flags >> 16};
             tiles += (uint32_t)G;
             units += j.n_patterns;
             // the launch stages with the largest hint of its batches
@@ -690,7 +713,7 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
         }
         if (grp.n == 0) continue;
         const fmx_status st = dev_err(timed(ix, "locate", s, units, [&] {
-            return launch_locate_group(ix, grp, stage, s);
+            return launch_locate_group(ix, grp, stage, status, s);
         }));
         if (st) return st;
     }
@@ -699,6 +722,7 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
 
 fmx_status fmx_sync(fmx_index *ix, void *stream) {
     if (!ix) return FMX_E_ARG;
+    DeviceGuard dg(ix->device);
     return read_status(ix, stream ? (hipStream_t)stream : ix->stream);
 }
 
@@ -734,7 +758,7 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     std::lock_guard<std::mutex> g(ix->mu);
     fmx_status st = check_patterns(offsets, n);
     if (st) return st;
-    hipSetDevice(ix->device);
+    DeviceGuard dg(ix->device);
     const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
     const uint64_t o_off = align_up(nb, 256), o_cnt = o_off + align_up((n + 1) * 8, 256);
     st = ensure_scratch(ix, o_cnt + n * pb);
@@ -755,11 +779,7 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
 static fmx_status ensure_ws(fmx_index *ix, uint64_t n) {
     const uint64_t need = ws_bytes_for(ix, n);
     if (ix->ws_bytes >= need) return FMX_OK;
-    if (ix->d_ws) {
-        hipFree(ix->d_ws);
-        std::lock_guard<std::mutex> g(ix->ws_mu);
-        ix->ws_state.erase(ix->d_ws);
-    }
+    if (ix->d_ws) hipFree(ix->d_ws);
     ix->d_ws = nullptr;
     ix->ws_bytes = 0;
     const uint64_t want = std::max<uint64_t>(need, 1 << 16);
@@ -778,7 +798,7 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
     std::lock_guard<std::mutex> g(ix->mu);
     fmx_status st = check_patterns(offsets, n);
     if (st) return st;
-    hipSetDevice(ix->device);
+    DeviceGuard dg(ix->device);
     const uint64_t nb = offsets[n], pb = ix->bv.L.pos_bytes;
     flags = (flags & 0xffu) | stage_hint(offsets, n);
     st = ensure_ws(ix, n);
@@ -830,6 +850,7 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
 fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
     if (!ix) return FMX_E_ARG;
     if (enable < 0) return FMX_E_ARG;
+    std::lock_guard<std::mutex> g(ix->timing_mu);
     ix->timing = enable != 0;
     ix->timing_every = enable > 0 ? (uint32_t)enable : 1u;
     ix->timing_seq = 0;
@@ -838,6 +859,7 @@ fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
 
 fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entries, int *n_entries) {
     if (!ix || !n_entries) return FMX_E_ARG;
+    std::lock_guard<std::mutex> g(ix->timing_mu);
     for (auto &t : ix->timers) {
         for (size_t i = 0; i < t.pending.size(); ++i) {
             auto &p = t.pending[i];
@@ -884,7 +906,8 @@ fmx_status fmx_build_device(const uint8_t *d_text, uint64_t text_len, const uint
                             fmx_layout layout, uint32_t kmer_size, uint32_t sampling_ratio, uint8_t *d_blob,
                             uint64_t blob_len, int device) {
     if (!d_blob || (text_len && !d_text)) return FMX_E_ARG;
-    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    DeviceGuard dg(device);
+    if (!dg.ok) return FMX_E_DEVICE;
     hipStream_t s;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
     fmx_status st = build_device(d_text, text_len, table, symbol_count, layout, kmer_size, sampling_ratio, d_blob,
@@ -899,7 +922,8 @@ fmx_status fmx_build(const uint8_t *text, uint64_t text_len, const uint8_t *tabl
                      uint64_t blob_len, int device) {
     if (!blob || (text_len && !text)) return FMX_E_ARG;
     if (((uintptr_t)blob) % align_of(layout) != 0) return FMX_E_ALIGN;  // BuildError::NotAlignedBlob
-    if (hipSetDevice(device) != hipSuccess) return FMX_E_DEVICE;
+    DeviceGuard dg(device);
+    if (!dg.ok) return FMX_E_DEVICE;
     uint8_t *dt = nullptr, *db = nullptr;
     if (hipMalloc(&dt, std::max<uint64_t>(text_len, 1)) != hipSuccess) return FMX_E_DEVICE;
     if (hipMalloc(&db, std::max<uint64_t>(blob_len, 16)) != hipSuccess) { hipFree(dt); return FMX_E_DEVICE; }

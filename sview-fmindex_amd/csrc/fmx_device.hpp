@@ -114,35 +114,97 @@ FMX_HD uint64_t sr_div(const QueryArgs &a, uint64_t pos, uint64_t &rem) {
 
 // ------------------------------------------------------- occ access (rank)
 
+using V4 = uint32_t __attribute__((ext_vector_type(4)));
+
 // REC == 0 — blob layout: rank_checkpoints [P; blocks*sigma] and blocks
 //            [BlockN<V>; blocks] are separate arrays (bwm/mod.rs:145-190).
-// REC > 0  — interleaved layout: record q (REC = 64 or 128 bytes, aligned) is
-//            [ckpt[0..sigma) as P][pad][bit planes at REC - N*VB/8], so one
-//            LF step reads one HBM line.
+// REC > 0  — interleaved layout (FMX_OCC_INTERLEAVED): record q (REC = 64 or
+//            128 bytes, REC-aligned) holds block q's N bit planes verbatim at
+//            [0, PB), then its sigma rank checkpoints as P at PBA + c*P (PBA =
+//            PB rounded up to P), zero padding to REC.  A rank query of
+//            symbol c reads the planes' 16-B chunks and the one chunk holding
+//            checkpoint c — all inside the record's line; when PB is not a
+//            multiple of 16 the planes' last chunk already holds the first
+//            checkpoints (C2, Block3<u64>, u32: 2 chunks for c < 2, 3 else).
 template <typename P, int N, int VB, int REC>
 struct Occ {
-    static constexpr int PLANE_BYTES = N * VB / 8;
-    static constexpr int PLANE_OFF = REC - PLANE_BYTES;
-    static constexpr int NCK = REC == 0 ? (1 << N) : PLANE_OFF / (int)sizeof(P);  // checkpoint slots
+    static constexpr int PB = N * VB / 8;                                      // plane bytes
+    static constexpr int PBA = (PB + (int)sizeof(P) - 1) / (int)sizeof(P) * (int)sizeof(P);
+    static constexpr int PBC = (PB + 15) / 16;                                 // chunks holding planes
+    static constexpr int NCH = REC / 16;                                       // chunks per record
+    static constexpr int NCK = REC == 0 ? (1 << N) : (REC - PBA) / (int)sizeof(P);  // checkpoint slots
     static constexpr int NCK2 = pow2_ceil(NCK);
+    static_assert(REC == 0 || PBA + (int)sizeof(P) <= REC, "record too small");
+
+    // One block's planes and one checkpoint, as read for a rank query.
+    struct Rec {
+        Planes<N, VB> pl;
+        P ck;
+    };
+
+    // dword d of a record's chunk array (d known at compile time after unrolling)
+    FMX_HD static uint32_t dw(const V4 *ch, int d) { return ch[d >> 2][d & 3]; }
+
+    FMX_HD static void planes_from(const V4 *ch, Planes<N, VB> &pl) {
+        using W = typename VecT<VB>::W;
+#pragma unroll
+        for (int w = 0; w < Planes<N, VB>::WORDS; ++w) {
+            if constexpr (sizeof(W) == 8) pl.w[w] = (uint64_t)dw(ch, 2 * w) | (uint64_t)dw(ch, 2 * w + 1) << 32;
+            else pl.w[w] = dw(ch, w);
+        }
+    }
+
+    // P at dword offset d (runtime, 0..3; P = u64: 0 or 2) of chunk v
+    FMX_HD static P pick(const V4 &v, uint32_t d) {
+        if constexpr (sizeof(P) == 8) return (P)(d & 2 ? (uint64_t)v[2] | (uint64_t)v[3] << 32
+                                                       : (uint64_t)v[0] | (uint64_t)v[1] << 32);
+        else return (P)(d & 2 ? (d & 1 ? v[3] : v[2]) : (d & 1 ? v[1] : v[0]));
+    }
+
+    // The planes of block q and checkpoint c (rank_checkpoints[q*sigma + c]).
+    FMX_HD static Rec fetch(const QueryArgs &a, uint64_t q, uint32_t c) {
+        Rec r;
+        if constexpr (REC == 0) {
+            r.ck = reinterpret_cast<const P *>(a.ckpt)[q * a.sigma + c];
+            r.pl.load(a.blocks + q * PB);
+        } else {
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * REC);
+            V4 ch[PBC];
+#pragma unroll
+            for (int i = 0; i < PBC; ++i) ch[i] = rp[i];
+            planes_from(ch, r.pl);
+            const uint32_t o = (uint32_t)PBA + c * (uint32_t)sizeof(P);
+            V4 cv;
+            if constexpr (PB % 16 != 0) {
+                cv = ch[PBC - 1];
+                if ((o >> 4) != (uint32_t)(PBC - 1)) cv = rp[o >> 4];
+            } else {
+                cv = rp[o >> 4];
+            }
+            r.ck = pick(cv, (o >> 2) & 3u);
+        }
+        return r;
+    }
 
     // Occ(c, stored position p): BwmView::get_next_rank after the sentinel
     // adjustment (bwm/mod.rs:206-214).  c is known before the loads, so only
     // the planes and the one checkpoint are fetched, all independently.
     FMX_HD static P rank_at(const QueryArgs &a, P p, uint32_t c) {
-        const uint64_t q = (uint64_t)p / VB;
-        const uint32_t rem = (uint32_t)((uint64_t)p % VB);
-        Planes<N, VB> pl;
-        P ck;
-        if constexpr (REC == 0) {
-            ck = reinterpret_cast<const P *>(a.ckpt)[q * a.sigma + c];
-            pl.load(a.blocks + q * PLANE_BYTES);
-        } else {
-            const uint8_t *r = a.occ + q * REC;
-            ck = reinterpret_cast<const P *>(r)[c];
-            pl.load(r + PLANE_OFF);
-        }
-        return ck + (P)pl.rank(rem, c);
+        const Rec r = fetch(a, (uint64_t)p / VB, c);
+        return r.ck + (P)r.pl.rank((uint32_t)((uint64_t)p % VB), c);
+    }
+
+    // Both rank queries of one LF step, Occ(c, plo) and Occ(c, phi)
+    // (next_pos_range, locate/mod.rs:39-45): when the two stored positions
+    // fall in the same block — every step once the interval is narrower than
+    // a block — that block is read once.
+    FMX_HD static void rank_pair(const QueryArgs &a, P plo, P phi, uint32_t c, P &rlo, P &rhi) {
+        const uint64_t ql = (uint64_t)plo / VB, qh = (uint64_t)phi / VB;
+        const Rec rl = fetch(a, ql, c);
+        Rec rh = rl;
+        if (qh != ql) rh = fetch(a, qh, c);
+        rlo = rl.ck + (P)rl.pl.rank((uint32_t)((uint64_t)plo % VB), c);
+        rhi = rh.ck + (P)rh.pl.rank((uint32_t)((uint64_t)phi % VB), c);
     }
 
     // get_pre_rank_and_symidx body (bwm/mod.rs:223-235) for stored position p:
@@ -154,7 +216,7 @@ struct Occ {
         const uint32_t rem = (uint32_t)((uint64_t)p % VB);
         Planes<N, VB> pl;
         if constexpr (REC == 0) {
-            pl.load(a.blocks + q * PLANE_BYTES);
+            pl.load(a.blocks + q * PB);
             const P *ckq = reinterpret_cast<const P *>(a.ckpt) + q * a.sigma;
             if constexpr (N <= 3) {
                 P all[NCK2];
@@ -167,17 +229,54 @@ struct Occ {
                 return ckq[c] + (P)pl.rank(rem, c);
             }
         } else {
-            const uint8_t *r = a.occ + q * REC;
-            P all[NCK2];
-            const P *ckr = reinterpret_cast<const P *>(r);
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * REC);
+            V4 ch[NCH];
 #pragma unroll
-            for (int i = 0; i < NCK2; ++i) all[i] = i < NCK ? ckr[i] : P(0);
-            pl.load(r + PLANE_OFF);
+            for (int i = 0; i < NCH; ++i) ch[i] = rp[i];
+            planes_from(ch, pl);
             c = pl.sym(rem);
+            P all[NCK2];
+#pragma unroll
+            for (int i = 0; i < NCK2; ++i) {
+                const int o = PBA + i * (int)sizeof(P);
+                if (i >= NCK) all[i] = P(0);
+                else if constexpr (sizeof(P) == 8) all[i] = (P)((uint64_t)dw(ch, o / 4) | (uint64_t)dw(ch, o / 4 + 1) << 32);
+                else all[i] = (P)dw(ch, o / 4);
+            }
             return tree_pick<NCK2>(all, c) + (P)pl.rank(rem, c);
         }
     }
 };
+
+// Interleaved record bytes for a layout (0: too wide, stay on the blob layout).
+FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits, uint32_t sigma) {
+    const uint32_t pb = planes * vec_bits / 8;
+    const uint32_t pba = (pb + pos_bytes - 1) / pos_bytes * pos_bytes;
+    const uint32_t need = pba + sigma * pos_bytes;
+    return need <= 64 ? 64u : need <= 128 ? 128u : 0u;
+}
+
+// Record q of the interleaved layout from the blob's block q (PB bytes of
+// planes) and its checkpoint row (sigma P's): k_relayout, and the CPU
+// emulation's copy (tests/emu).
+template <typename P, int N, int VB, int REC>
+FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckrow, uint32_t sigma) {
+    using O = Occ<P, N, VB, REC>;
+    uint32_t w[REC / 4];
+#pragma unroll
+    for (int i = 0; i < REC / 4; ++i) w[i] = 0;
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(planes);
+#pragma unroll
+    for (int i = 0; i < O::PB / 4; ++i) w[i] = pw[i];
+    const uint32_t *cw = reinterpret_cast<const uint32_t *>(ckrow);
+    const uint32_t ncw = sigma * (uint32_t)(sizeof(P) / 4);
+#pragma unroll
+    for (int i = 0; i < (REC - O::PBA) / 4; ++i)
+        if ((uint32_t)i < ncw) w[O::PBA / 4 + i] = cw[i];
+    V4 *d = reinterpret_cast<V4 *>(dst);
+#pragma unroll
+    for (int i = 0; i < REC / 16; ++i) d[i] = V4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+}
 
 // ----------------------------------------------------- shared kernel parts
 
@@ -187,6 +286,7 @@ struct Tables {
     uint8_t dig[kMaxSigma];  // symbol -> deep-table digit (QueryArgs::dlut_dig)
     P C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
+    const P *kt;  // the blob's k-mer count table: a workgroup's LDS copy, or the blob itself
 };
 
 // One pattern, position j = 0..m-1 in pattern order.  Either staged: the
@@ -463,7 +563,12 @@ FMX_HD bool dlut_code(const QueryArgs &a, const Tables<P> &s, const PatView &pv,
     return !miss;
 }
 
-template <typename P, int N, int VB, int REC, bool LT = false>
+// Kernel variants of the search (template parameter VAR):
+constexpr int kVarFaithful = 0;  // the blob's structures only (+ FMX_OCC_INTERLEAVED): no derived-index code
+constexpr int kVarDerived = 1;   // derived structures, short single-row tail compares
+constexpr int kVarDerivedLong = 2;  // derived structures, vectorised long tail compares
+
+template <typename P, int N, int VB, int REC, int VAR = kVarDerived>
 FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatView &pv, bool have, P w0, P w1,
                               P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode);
 
@@ -472,27 +577,32 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
 // mode kHitRows, or (derived structures) an interval finished early: a
 // single row checked against the text (kHitOne), or a row-context scan
 // (kHitOne / kHitMask, see scan_rows).  The count is always hi - lo.
-template <typename P, int N, int VB, int REC, bool LT = false>
+template <typename P, int N, int VB, int REC, int VAR = kVarDerived>
 FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv, P &lo, P &hi, P &rloc,
                        uint64_t &mask, uint32_t &mode) {
-    uint64_t code;
-    const bool have = dlut_code<P>(a, s, pv, code);
-    P w0 = 0, w1 = 0;
-    if (have) {
-        const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
-        w0 = dl[0];
-        w1 = dl[1];
+    if constexpr (VAR == kVarFaithful) {
+        return search_seeded<P, N, VB, REC, VAR>(a, s, pv, false, P(0), P(0), lo, hi, rloc, mask, mode);
+    } else {
+        uint64_t code;
+        const bool have = dlut_code<P>(a, s, pv, code);
+        P w0 = 0, w1 = 0;
+        if (have) {
+            const P *dl = reinterpret_cast<const P *>(a.dlut) + 2 * code;
+            w0 = dl[0];
+            w1 = dl[1];
+        }
+        return search_seeded<P, N, VB, REC, VAR>(a, s, pv, have, w0, w1, lo, hi, rloc, mask, mode);
     }
-    return search_seeded<P, N, VB, REC, LT>(a, s, pv, have, w0, w1, lo, hi, rloc, mask, mode);
 }
 
 // search() after the deep-table read: `have` = the entry {w0, w1} of the
 // pattern's last K symbols (the interval K-k more LF steps from the blob's
 // seed reach, or a single-row entry) was read.
-template <typename P, int N, int VB, int REC, bool LT>
+template <typename P, int N, int VB, int REC, int VAR>
 FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatView &pv, bool have, P w0, P w1,
                               P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode) {
     using O = Occ<P, N, VB, REC>;
+    constexpr bool LT = VAR == kVarDerivedLong, DER = VAR != kVarFaithful;
     const uint32_t sigma = a.sigma, k = a.k;
     const uint64_t m = pv.m;
     const P sent = (P)a.sentinel;
@@ -504,7 +614,7 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
     uint64_t idx = 0;
     uint32_t bad = 0;
     bool seeded = false;
-    if (have) {
+    if (DER && have) {
         idx = m - a.dlut_k;
         if (a.dlut_rows && (w0 & row_flag<P>())) return one_row<P, LT>(a, pv, idx, w0, w1, lo, hi, rloc, mode);
         lo = w0;
@@ -523,41 +633,42 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
         if (bad) return kStatusSymbol;
         if (m < k) { e = code + s.mult[m - 1] - 1; idx = 0; }
         else { e = code; idx = m - k; }
-        const P *kt = reinterpret_cast<const P *>(a.kmer);
-        lo = kt[code - 1];
-        hi = kt[e];
+        lo = s.kt[code - 1];
+        hi = s.kt[e];
     }
     // a PassThrough pattern with a byte >= sigma must reach it in the LF loop
-    bool scan = a.ctx_len != 0;
+    bool scan = DER && a.ctx_len != 0;
     if (scan && a.strict)
         for (uint64_t j = 0; j < idx; ++j) scan &= pv.at(j) < sigma;
     // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
     uint32_t c = idx > 0 ? pv.at(idx - 1) : 0;  // next symbol, fetched one step ahead
     while (lo < hi && idx > 0) {
-        if (scan && hi - lo <= (P)a.scan_rows) {
-            scan_rows<P, LT>(a, pv, idx, lo, hi, rloc, mask, mode);
-            return 0;
-        }
-        if (a.text != nullptr && hi - lo == P(1)) {
-            const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[(uint64_t)lo * a.sa_stride];
-            const int64_t jm = tail_mismatch<LT>(a.text, pv, idx, x, idx);
-            mode = kHitOne;
-            if (jm >= 0) {
-                // the LF loop reads (and would reject) the symbol at jm before
-                // the interval empties there
-                if (pv.at((uint64_t)jm) >= sigma) { lo = hi = 0; return kStatusSymbol; }
-                hi = lo;
-            } else {
-                rloc = (P)(x - idx);
+        if constexpr (DER) {
+            if (scan && hi - lo <= (P)a.scan_rows) {
+                scan_rows<P, LT>(a, pv, idx, lo, hi, rloc, mask, mode);
+                return 0;
             }
-            return 0;
+            if (a.text != nullptr && hi - lo == P(1)) {
+                const uint64_t x = (uint64_t)reinterpret_cast<const P *>(a.safull)[(uint64_t)lo * a.sa_stride];
+                const int64_t jm = tail_mismatch<LT>(a.text, pv, idx, x, idx);
+                mode = kHitOne;
+                if (jm >= 0) {
+                    // the LF loop reads (and would reject) the symbol at jm before
+                    // the interval empties there
+                    if (pv.at((uint64_t)jm) >= sigma) { lo = hi = 0; return kStatusSymbol; }
+                    hi = lo;
+                } else {
+                    rloc = (P)(x - idx);
+                }
+                return 0;
+            }
         }
         idx -= 1;
         if (c >= sigma) { lo = hi = 0; return kStatusSymbol; }
         const P plo = lo + (lo < sent ? P(1) : P(0));  // bwm/mod.rs:202-204
         const P phi = hi + (hi < sent ? P(1) : P(0));
-        const P rlo = O::rank_at(a, plo, c);
-        const P rhi = O::rank_at(a, phi, c);
+        P rlo, rhi;
+        O::rank_pair(a, plo, phi, c, rlo, rhi);
         const P pre = s.C[c];
         c = idx > 0 ? pv.at(idx - 1) : 0;
         lo = pre + rlo;

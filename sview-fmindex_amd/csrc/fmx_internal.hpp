@@ -75,7 +75,7 @@ struct QueryArgs {
     uint32_t sa_stride;       // 1: plain full SA; 2: row records {SA[r], ctx[r]} (FMX_OPT_ROW_CONTEXT)
     uint32_t ctx_len;         // symbols per row context (0: no contexts)
     uint32_t scan_rows;       // intervals of at most this many rows are finished by a record scan
-    uint32_t pad2_;
+    uint32_t kt_lds_bytes;    // k-mer count table bytes when a workgroup copies it into LDS (else 0)
     uint64_t wpow[65];        // (sigma+1)^i, i <= ctx_len
     uint64_t C[kMaxSigma + 1];
     uint64_t mult[kMaxK];
@@ -85,11 +85,12 @@ struct QueryArgs {
 };
 
 constexpr uint8_t kNoDigit = 0xFF;
+constexpr uint32_t kStatusSlots = 1024;   // status words per index (one per stream)
+constexpr uint64_t kKmerLdsMax = 4096;    // k-mer count tables up to this size are staged in LDS
 
 // Device status bits
 constexpr uint32_t kStatusEmpty = 1u;
 constexpr uint32_t kStatusSymbol = 2u;
-constexpr uint32_t kStatusHang = 4u;  // a bounded look-back spin gave up
 constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
 
 struct Timer {
@@ -115,16 +116,16 @@ struct fmx_index {
     uint64_t occ_bytes = 0;
     uint32_t occ_mode = FMX_OCC_BLOB;
     uint32_t rec_bytes = 0;
-    uint32_t *d_status = nullptr;
+    uint32_t *d_status = nullptr;  // kStatusSlots words: one per stream launched on
+    std::unordered_map<const void *, uint32_t *> status_of;
+    uint32_t status_used = 0;
+    std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
     uint8_t *d_safull = nullptr;
     uint64_t safull_bytes = 0;
     uint8_t *d_text = nullptr;
     uint32_t options = 0;
-    bool tile_pairs = false;  // FMX_TILE_PAIRS=1: k_search2 (two tiles per workgroup, entry reads paired)
-    bool locate_fused = false;  // FMX_LOCATE_FUSED=1: the single-kernel k_locate (look-back) instead of
-                                // k_search + k_scan + k_emit
     fmx::QueryArgs qa{};
     // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
@@ -135,37 +136,25 @@ struct fmx_index {
     bool timing = false;
     uint32_t timing_every = 1;   // bracket every k-th launch
     uint64_t timing_seq = 0;
-    // k_locate look-back state per caller workspace: the last epoch handed
-    // out, and the most tiles ever published on it (what a wrap must clear)
-    struct WsState {
-        uint32_t epoch = 0;
-        uint64_t hi_tiles = 0;
-    };
-    std::unordered_map<const void *, WsState> ws_state;
-    std::mutex ws_mu;
     std::vector<fmx::Timer> timers;
     std::vector<hipEvent_t> event_pool;
-    std::mutex mu;
+    std::mutex timing_mu;  // timers, event_pool, timing_seq
+    std::mutex mu;         // the host-buffer calls' scratch and workspace
 };
 
 namespace fmx {
 
 // Query launchers (fmx_query.hip).  All asynchronous on `stream`.
 hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
-                        uint32_t flags, void *d_counts, hipStream_t stream);
-// Count + offsets scan + locate: k_search, k_scan, k_emit (or, with
-// FMX_LOCATE_FUSED=1, the single-kernel k_locate).  d_ctl (2 x u32) and d_tiles must be zero before
-// their first use.  k_locate: d_tiles holds tiles_cap epoch-tagged look-back
-// words, epoch in 1..kLocateEpochs (fmx_api.cpp hands them out per workspace);
-// split: d_tiles = [tile counts][tile offsets][n search records], d_ctl its
-// finished-workgroup counter, reset by the kernel.
+                        uint32_t flags, void *d_counts, uint32_t *status, hipStream_t stream);
+// Count + offsets scan + locate: k_search, (k_scan,) k_emit.  d_tiles =
+// [tile counts: G][tile offsets: G][n search records] (G = ceil(n / 256)).
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                          uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
-                         uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
-                         uint32_t epoch, hipStream_t stream);
-constexpr uint32_t kLocateEpochs = 63;  // k_locate tile words carry 6 bits of epoch
-// One batch of a k_locate launch; a launch runs up to kMaxGroup of them, each
-// with its own patterns, outputs and look-back tiles (fmx_locate_group_async).
+                         uint64_t *d_needed, uint64_t *d_tiles, uint64_t tiles_cap, uint32_t *status,
+                         hipStream_t stream);
+// One batch of a locate launch; a launch runs up to kMaxGroup of them, each
+// with its own patterns, outputs and workspace (fmx_locate_group_async).
 constexpr uint32_t kMaxGroup = 8;
 struct LocateBatch {
     const uint8_t *bytes;
@@ -177,7 +166,6 @@ struct LocateBatch {
     uint64_t cap;
     uint64_t *needed;
     uint64_t *tiles;
-    uint32_t epoch;
     uint32_t rev;
     uint32_t stride;  // FMX_HINT_FIXED_LEN: offs[i] == i * stride (0: read the offsets)
 };
@@ -187,7 +175,7 @@ struct LocateGroup {
     uint32_t n;
 };
 hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
-                               hipStream_t stream);
+                               uint32_t *status, hipStream_t stream);
 uint64_t locate_tiles_cap(uint64_t n);
 // Bytes per pattern of the search-result records in the locate workspace.
 uint64_t locate_rec_bytes(uint32_t pos_bytes);

@@ -5,21 +5,23 @@
 //                next_pos_range, src/locate/mod.rs:38-45;
 //                BwmView::get_next_rank, components/bwm/mod.rs:197-215;
 //                CountArrayView seed, components/count_array.rs:203-233)
-//   k_locate  : one launch for a whole count+locate batch: the k_count body,
-//               then a single-pass decoupled look-back scan of the counts
-//               (output offsets), then the sampled-SA locate walk of every
-//               occurrence row, rows dealt across the 64 lanes of a wavefront
+//   k_search  : the same search for a locate batch; a pattern whose interval
+//               is one row walks that row to its sampled SA entry right away
 //               (write_locations_to_buffer, src/locate/mod.rs:14-37;
 //                get_pre_rank_and_symidx, components/bwm/mod.rs:217-236;
 //                SuffixArrayView::get_location_of, suffix_array/mod.rs:100-105)
+//               and leaves a search record per pattern plus its tile's count
+//   k_scan    : tile offsets of batches too large for k_emit's own sum
+//   k_emit    : output offsets, then every location: settled ones copied,
+//               the rows of multi-row intervals walked, dealt across the 64
+//               lanes of a wavefront
 //   k_relayout: optional one-time re-layout of (rank checkpoints, bit planes)
 //               into one HBM record per block (FMX_OCC_INTERLEAVED).
 //
 // All integer work: no MFMA.  The hot loop is a chain of dependent random
 // gathers, so the kernels keep many independent chains (lanes) in flight and
-// make each LF step cost one HBM round trip: the checkpoint and bit-plane loads
-// of a step are independent of each other, and in the interleaved layout they
-// are the same line.
+// make each LF step cost one record read per rank query — one for both when
+// lo and hi share a block.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -28,29 +30,25 @@
 
 namespace fmx {
 
-#ifdef FMX_PHASE_STAMPS
-// Diagnostic build only: s_memrealtime (100 MHz) per wave at each phase of
-// k_locate: [0] entry, [6] tile id known, [7] pattern offsets loaded,
-// [1] patterns staged, [2] search done, [3] offsets known (look-back done),
-// [4] locations written, [5] tile id.
-constexpr uint32_t kStampWaves = 1u << 17, kStampSlots = 8;
-__device__ uint64_t g_stamps[kStampWaves * kStampSlots];
-#define FMX_STAMP(slot, v)                                                                   \
-    do {                                                                                     \
-        const uint32_t wv_ = blockIdx.x * 4u + (threadIdx.x >> 6);                           \
-        if ((threadIdx.x & 63) == 0 && wv_ < kStampWaves) g_stamps[wv_ * kStampSlots + (slot)] = (v); \
-    } while (0)
-#else
-#define FMX_STAMP(slot, v) do { } while (0)
-#endif
-
+// The per-workgroup tables: encoding table, C array, k-mer multipliers, and
+// — when it is small (QueryArgs::kt_lds_bytes) — the blob's k-mer count
+// table, copied into LDS at `kt_lds` so that the seed's two reads are LDS
+// reads.  Visible after the caller's next barrier.
 template <typename P>
-__device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s) {
+__device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s, uint8_t *kt_lds) {
     const int t = threadIdx.x;
     s.enc[t] = a.enc[t];
     if (t < kMaxSigma) s.dig[t] = a.dlut_dig[t];
     if ((uint32_t)t <= a.sigma) s.C[t] = (P)a.C[t];
     if ((uint32_t)t < a.k) s.mult[t] = a.mult[t];
+    if (a.kt_lds_bytes && kt_lds) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.kmer);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(kt_lds);
+        for (uint32_t i = t; i < a.kt_lds_bytes / 4; i += 256) dst[i] = src[i];
+        if (t == 0) s.kt = reinterpret_cast<const P *>(kt_lds);
+    } else if (t == 0) {
+        s.kt = reinterpret_cast<const P *>(a.kmer);
+    }
 }
 
 // 256-thread workgroup exclusive scan of one u64 per thread.
@@ -119,10 +117,6 @@ __device__ __forceinline__ bool stage_span(const Tables<P> &s, uint8_t *s_pat, c
         }
     }
     const uint64_t len = b1 - b0;
-#ifdef FMX_PHASE_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    FMX_STAMP(7, __builtin_amdgcn_s_memrealtime() + (beg[0] & 0) + (end[0] & 0) + (len & 0));
-#endif
     uint32_t bad_stride = 0;
 #pragma unroll
     for (int q = 0; q < NP; ++q) bad_stride |= chk[q] != end[q];
@@ -185,13 +179,13 @@ __device__ __forceinline__ PatView pattern_view(const Tables<P> &s, const uint8_
     return pv;
 }
 
-template <typename P, int N, int VB, int REC, bool LT>
+template <typename P, int N, int VB, int REC, int VAR>
 __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
                                                const uint64_t *__restrict__ offs, uint64_t npat,
                                                uint32_t flags, P *__restrict__ out_cnt, uint32_t stage_bytes) {
     __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
-    stage_tables(a, s);
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    stage_tables(a, s, s_pat + stage_bytes);
     __syncthreads();
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
     const uint64_t first = (uint64_t)blockIdx.x * 256u;
@@ -205,12 +199,12 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
     P lo, hi, rloc;
     uint64_t mask;
     uint32_t mode;
-    const uint32_t bad = search<P, N, VB, REC, LT>(a, s, pv, lo, hi, rloc, mask, mode);
+    const uint32_t bad = search<P, N, VB, REC, VAR>(a, s, pv, lo, hi, rloc, mask, mode);
     if (bad) atomicOr(a.status, bad);
     out_cnt[i] = hi - lo;
 }
 
-// ---------------------------------------------------------------- k_locate
+// ------------------------------------------------------------ locations
 
 // The locations of a wave's 64 patterns (lane j: pattern with output slots
 // [my_off, my_off + cnt) and its search result), every occurrence row dealt
@@ -256,150 +250,6 @@ __device__ __forceinline__ void emit_locations(const QueryArgs &a, const P *C, u
 }
 
 
-// Look-back tile word: (sum << 8) | (epoch << 2) | flag, sum = the tile's
-// aggregate (kTileAgg) or inclusive prefix (kTileInc).  A word whose epoch is
-// not this launch's is unpublished: the workspace needs no clearing between
-// launches, and no workgroup has to learn that it is the last one out (that
-// took one same-address device-scope atomic per workgroup, serialised across
-// the XCDs, at the tail of every launch).  The host hands out epochs
-// 1..kLocateEpochs per workspace and zeroes the used tiles before reusing 1.
-constexpr uint64_t kTileAgg = 1, kTileInc = 2;
-
-template <typename P, int N, int VB, int REC, bool LT>
-__global__ __launch_bounds__(256, LT ? 4 : 8) void k_locate(const QueryArgs a, const LocateGroup grp, uint32_t stage_bytes) {
-    __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
-    __shared__ uint64_t s_scan[4];
-    __shared__ uint64_t s_prefix;
-    FMX_STAMP(0, __builtin_amdgcn_s_memrealtime());
-    stage_tables(a, s);
-    // This workgroup's batch (workgroup-uniform: scalar kernel-argument reads).
-    uint32_t jb = 0;
-#pragma unroll
-    for (uint32_t t = 1; t < kMaxGroup; ++t)
-        if (t < grp.n && blockIdx.x >= grp.tile_begin[t]) jb = t;
-    const LocateBatch &B = grp.b[jb];
-    const uint8_t *__restrict__ bytes = B.bytes;
-    const uint64_t *__restrict__ offs = B.offs;
-    const uint64_t npat = B.npat;
-    P *__restrict__ out_cnt = (P *)B.out_cnt;
-    uint64_t *__restrict__ loc_off = B.loc_off;
-    P *__restrict__ out_locs = (P *)B.out_locs;
-    const uint64_t cap = B.cap;
-    uint64_t *__restrict__ needed = B.needed;
-    uint64_t *__restrict__ tiles = B.tiles;
-    const uint32_t epoch = B.epoch;
-    const uint32_t G = (uint32_t)((npat + 255) / 256);
-    // Tile g of the batch.  The look-back below waits only on lower tiles of
-    // the same batch, and workgroups are dispatched in increasing id order
-    // (per XCD, round-robin over XCDs), so every tile waited on is running or
-    // done.  (A ticket taken with one device-scope atomic per workgroup would
-    // guarantee the same at the price of serialised atomics on one address
-    // before any pattern is read — 5-10 us of a 30 us launch, measured.)
-    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
-    FMX_STAMP(6, __builtin_amdgcn_s_memrealtime());
-
-    // ---- 1. SA interval of every pattern of the tile ----------------------
-    const bool rev = B.rev != 0;
-    uint64_t beg, end, b0, b1;
-    const bool staged =
-        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, B.stride, a.status,
-                       beg, end, b0, b1);
-    __syncthreads();
-    FMX_STAMP(1, __builtin_amdgcn_s_memrealtime());
-    FMX_STAMP(5, g);
-    const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
-    P lo = 0, hi = 0, rloc = 0;
-    uint64_t mask = 0;
-    uint32_t mode = kHitRows;
-    if (i < npat) {
-        const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
-        const uint32_t bad = search<P, N, VB, REC, LT>(a, s, pv, lo, hi, rloc, mask, mode);
-        if (bad) atomicOr(a.status, bad);
-        if (out_cnt) out_cnt[i] = hi - lo;
-    }
-    const uint64_t cnt = (uint64_t)(hi - lo);
-    FMX_STAMP(2, __builtin_amdgcn_s_memrealtime());
-
-    // ---- 2. output offsets: single-pass scan with decoupled look-back -----
-    uint64_t agg;
-    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);
-    const uint64_t ep = (uint64_t)epoch << 2;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        if (g == 0) {
-            if (lane == 0) {
-                __hip_atomic_store(&tiles[0], (agg << 8) | ep | kTileInc, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                s_prefix = 0;
-            }
-        } else {
-            if (lane == 0)
-                __hip_atomic_store(&tiles[g], (agg << 8) | ep | kTileAgg, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t prefix = 0;
-            int64_t j = (int64_t)g - 1;
-            uint32_t spins = 0;
-            while (true) {
-                const int64_t idx = j - lane;
-                const uint64_t w = idx >= 0
-                    ? __hip_atomic_load(&tiles[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : (ep | kTileInc);  // before tile 0: an inclusive prefix of 0
-                const bool live = (w & 0xFCull) == ep && (w & 3) != 0;  // published by this launch
-                const uint64_t incm = __ballot(live && (w & 3) == kTileInc);
-                const uint64_t waitm = __ballot(!live);
-                const int first_inc = incm ? __builtin_ctzll(incm) : 64;
-                const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
-                if (waitm & upto) {
-                    // A predecessor has not published yet (it is still
-                    // searching).  Wait on that one word from one lane — a
-                    // 64-lane window re-read per round trip from every waiting
-                    // workgroup would take a large share of the chip's memory
-                    // requests — then read the window again.
-                    const int64_t widx = j - (int64_t)__builtin_ctzll(waitm & upto);
-                    uint64_t wv = 0;
-                    bool hang = false;
-                    do {
-                        __builtin_amdgcn_s_sleep(2);
-                        if (lane == 0)
-                            wv = __hip_atomic_load(&tiles[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        wv = __shfl(wv, 0);
-                        hang = ++spins > (1u << 24);
-                    } while (((wv & 0xFCull) != ep || (wv & 3) == 0) && !hang);
-                    if (hang) { if (lane == 0) atomicOr(a.status, kStatusHang); break; }
-                    continue;
-                }
-                uint64_t v = lane <= first_inc ? (w >> 8) : 0;
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d);
-                prefix += v;
-                if (first_inc < 64) break;
-                j -= 64;
-            }
-            if (lane == 0) {
-                __hip_atomic_store(&tiles[g], ((prefix + agg) << 8) | ep | kTileInc, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                s_prefix = prefix;
-            }
-        }
-    }
-    __syncthreads();
-    FMX_STAMP(3, __builtin_amdgcn_s_memrealtime());
-    const uint64_t my_off = s_prefix + excl;
-    if (i < npat) loc_off[i] = my_off;
-    if (g == G - 1 && threadIdx.x == 0) {
-        loc_off[npat] = s_prefix + agg;
-        *needed = s_prefix + agg;
-    }
-
-    // ---- 3. locate walk, rows of the wave's 64 patterns dealt to its lanes --
-    emit_locations<P, N, VB, REC>(a, s.C, my_off, cnt, lo, rloc, mask, mode, cap, out_locs);
-#ifdef FMX_PHASE_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
-    FMX_STAMP(4, __builtin_amdgcn_s_memrealtime());
-}
-
 // ------------------------------------------------- k_search + k_emit (split)
 
 // A pattern's search result, handed from k_search to k_emit (P-typed words):
@@ -433,7 +283,7 @@ __device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &
     return is_mask ? (uint64_t)__builtin_popcountll(x) : (uint64_t)r.b;
 }
 
-// The three-kernel locate (the default; FMX_LOCATE_FUSED=1 selects k_locate).
+// The locate launch: k_search, (k_scan,) k_emit.
 // No workgroup ever waits on another, so nothing depends on the order or
 // placement in which workgroups are dispatched (MI355X_MICROARCH.md: HIP
 // promises neither; a look-back that assumes in-order dispatch can deadlock
@@ -450,7 +300,7 @@ __device__ __forceinline__ uint32_t group_batch(const LocateGroup &grp, uint32_t
 }
 
 // 1. Search every pattern; its result record, its count; the tile's count.
-template <typename P, int N, int VB, int REC, bool LT>
+template <typename P, int N, int VB, int REC, int VAR>
 __device__ __forceinline__ void search_tile(const QueryArgs &a, const LocateGroup &grp, const Tables<P> &s,
                                             uint8_t *s_pat, uint64_t *s_scan, uint32_t stage_bytes, uint32_t vt) {
     const uint32_t jb = group_batch(grp, vt);
@@ -474,10 +324,17 @@ __device__ __forceinline__ void search_tile(const QueryArgs &a, const LocateGrou
         P lo, hi, rloc;
         uint64_t mask;
         uint32_t mode;
-        const uint32_t bad = search<P, N, VB, REC, LT>(a, s, pv, lo, hi, rloc, mask, mode);
+        const uint32_t bad = search<P, N, VB, REC, VAR>(a, s, pv, lo, hi, rloc, mask, mode);
         if (bad) atomicOr(a.status, bad);
         cnt = (uint64_t)(hi - lo);
         if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = hi - lo;
+        // one row (most patterns of a large text): its location now, while
+        // this lane's chain is live (locate/mod.rs:19-35); k_emit then only
+        // copies it
+        if (mode == kHitRows && cnt == 1) {
+            rloc = walk_row<P, N, VB, REC>(a, s.C, lo);
+            mode = kHitOne;
+        }
         recs[i] = pack_rec<P>(lo, hi, rloc, mask, mode);
     }
     uint64_t agg;
@@ -485,87 +342,14 @@ __device__ __forceinline__ void search_tile(const QueryArgs &a, const LocateGrou
     if (threadIdx.x == 0) B.tiles[g] = agg;
 }
 
-template <typename P, int N, int VB, int REC, bool LT>
-__global__ __launch_bounds__(256, LT ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
+template <typename P, int N, int VB, int REC, int VAR>
+__global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
                                                              uint32_t stage_bytes) {
     __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, dynamic
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
     __shared__ uint64_t s_scan[4];
-    stage_tables(a, s);
-    search_tile<P, N, VB, REC, LT>(a, grp, s, s_pat, s_scan, stage_bytes, blockIdx.x);
-}
-
-// k_search over a pair of tiles per workgroup (FMX_TILE_PAIRS=1): each lane
-// owns one pattern of each tile, the pair is staged as one span (one round
-// trip for the offsets, one for the bytes) and both patterns' deep-table
-// entries are read before either is used — twice the dependent requests in
-// flight per wave slot.  A pair split across two batches of a group (or a
-// lone last tile) runs tile by tile.  6 waves/SIMD (80 VGPRs): at 8 the
-// pair spilled 55 VGPRs.
-template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256, 6) void k_search2(const QueryArgs a, const LocateGroup grp,
-                                                    uint32_t stage_bytes, uint32_t ntiles) {
-    __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // 2 * stage_bytes, dynamic
-    __shared__ uint64_t s_scan[4];
-    stage_tables(a, s);
-    const uint32_t vt0 = 2u * blockIdx.x, vt1 = vt0 + 1u;
-    const uint32_t jb = group_batch(grp, vt0);
-    if (vt1 >= ntiles || group_batch(grp, vt1) != jb) {  // workgroup-uniform
-        search_tile<P, N, VB, REC, false>(a, grp, s, s_pat, s_scan, stage_bytes, vt0);
-        if (vt1 < ntiles) search_tile<P, N, VB, REC, false>(a, grp, s, s_pat, s_scan, stage_bytes, vt1);
-        return;
-    }
-    const LocateBatch &B = grp.b[jb];
-    const uint8_t *__restrict__ bytes = B.bytes;
-    const uint64_t npat = B.npat;
-    const bool rev = B.rev != 0;
-    const uint32_t g = vt0 - grp.tile_begin[jb];
-    const uint64_t G = (npat + 255) / 256;
-    SearchRec<P> *__restrict__ recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
-    uint64_t beg[2], end[2], b0, b1;
-    const bool staged = stage_span<P, 2>(s, s_pat, bytes, B.offs, npat, (uint64_t)g * 256u, rev, 2 * stage_bytes,
-                                         B.stride, a.status, beg, end, b0, b1);
-    __syncthreads();
-    const uint64_t i0 = (uint64_t)g * 256u + threadIdx.x, i1 = i0 + 256u;
-    const bool v0 = i0 < npat, v1 = i1 < npat;
-    const PatView pv0 = pattern_view(s, s_pat, staged, bytes, beg[0], end[0], b0, b1, rev);
-    const PatView pv1 = pattern_view(s, s_pat, staged, bytes, beg[1], end[1], b0, b1, rev);
-    uint64_t c0 = 0, c1 = 0;
-    const bool h0 = v0 && dlut_code<P>(a, s, pv0, c0);
-    const bool h1 = v1 && dlut_code<P>(a, s, pv1, c1);
-    const P *dl = reinterpret_cast<const P *>(a.dlut);
-    P w00 = 0, w01 = 0, w10 = 0, w11 = 0;
-    if (h0) { w00 = dl[2 * c0]; w01 = dl[2 * c0 + 1]; }
-    if (h1) { w10 = dl[2 * c1]; w11 = dl[2 * c1 + 1]; }
-    uint64_t cnt0 = 0, cnt1 = 0;
-    if (v0) {
-        P lo, hi, rloc;
-        uint64_t mask;
-        uint32_t mode;
-        const uint32_t bad = search_seeded<P, N, VB, REC, false>(a, s, pv0, h0, w00, w01, lo, hi, rloc, mask, mode);
-        if (bad) atomicOr(a.status, bad);
-        cnt0 = (uint64_t)(hi - lo);
-        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i0] = hi - lo;
-        recs[i0] = pack_rec<P>(lo, hi, rloc, mask, mode);
-    }
-    if (v1) {
-        P lo, hi, rloc;
-        uint64_t mask;
-        uint32_t mode;
-        const uint32_t bad = search_seeded<P, N, VB, REC, false>(a, s, pv1, h1, w10, w11, lo, hi, rloc, mask, mode);
-        if (bad) atomicOr(a.status, bad);
-        cnt1 = (uint64_t)(hi - lo);
-        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i1] = hi - lo;
-        recs[i1] = pack_rec<P>(lo, hi, rloc, mask, mode);
-    }
-    uint64_t agg0, agg1;
-    block_excl_scan(cnt0, &agg0, s_scan);
-    block_excl_scan(cnt1, &agg1, s_scan);
-    if (threadIdx.x == 0) {
-        B.tiles[g] = agg0;
-        B.tiles[g + 1] = agg1;
-    }
+    stage_tables(a, s, s_pat + stage_bytes);
+    search_tile<P, N, VB, REC, VAR>(a, grp, s, s_pat, s_scan, stage_bytes, blockIdx.x);
 }
 
 // 2. One workgroup per batch: exclusive scan of its tile counts into tile
@@ -712,7 +496,7 @@ template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_full_sa(const QueryArgs a, uint64_t n, P *__restrict__ sa_out,
                                                  uint32_t stride) {
     __shared__ Tables<P> s;
-    stage_tables(a, s);
+    stage_tables(a, s, nullptr);
     __syncthreads();
     QueryArgs b = a;
     b.safull = nullptr;
@@ -753,33 +537,16 @@ __global__ __launch_bounds__(256) void k_row_ctx(const QueryArgs a, uint64_t n, 
 
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_relayout(const QueryArgs a, uint64_t blocks_len, uint8_t *__restrict__ occ) {
-    constexpr int PB = N * VB / 8, POFF = REC - PB;
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= blocks_len) return;
-    uint32_t words[REC / 4];
-#pragma unroll
-    for (int i = 0; i < REC / 4; ++i) words[i] = 0;
-    const uint32_t *cp = reinterpret_cast<const uint32_t *>(a.ckpt + q * a.sigma * sizeof(P));
-    const uint32_t cw = a.sigma * (uint32_t)(sizeof(P) / 4);
-#pragma unroll
-    for (int i = 0; i < POFF / 4; ++i)
-        if ((uint32_t)i < cw) words[i] = cp[i];
-    const uint32_t *bp = reinterpret_cast<const uint32_t *>(a.blocks + q * PB);
-#pragma unroll
-    for (int i = 0; i < PB / 4; ++i) words[POFF / 4 + i] = bp[i];
-    uint4 *rp = reinterpret_cast<uint4 *>(occ + q * REC);
-#pragma unroll
-    for (int i = 0; i < REC / 16; ++i)
-        rp[i] = make_uint4(words[4 * i], words[4 * i + 1], words[4 * i + 2], words[4 * i + 3]);
+    write_record<P, N, VB, REC>(occ + q * REC, a.blocks + q * (N * VB / 8), a.ckpt + q * a.sigma * sizeof(P),
+                                a.sigma);
 }
 
 // ------------------------------------------------------------- dispatch
 
 uint32_t interleaved_record_bytes(const BlobView &bv) {
-    const uint32_t need = bv.L.planes * bv.L.vec_bits / 8 + bv.sigma * bv.L.pos_bytes;
-    if (need <= 64) return 64;
-    if (need <= 128) return 128;
-    return 0;  // too wide: stay on the blob layout
+    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma);
 }
 
 // Compile-time dispatch over the layout: F is a generic lambda called as
@@ -789,10 +556,10 @@ static hipError_t disp_rec(uint32_t rec, F &&f) {
     switch (rec) {
         case 0: return f.template operator()<P, N, VB, 0>();
         case 64:
-            if constexpr (N * VB / 8 + (int)sizeof(P) <= 64) return f.template operator()<P, N, VB, 64>();
+            if constexpr (Occ<P, N, VB, 0>::PBA + (int)sizeof(P) <= 64) return f.template operator()<P, N, VB, 64>();
             else return hipErrorInvalidValue;
         case 128:
-            if constexpr (N * VB / 8 + (int)sizeof(P) <= 128) return f.template operator()<P, N, VB, 128>();
+            if constexpr (Occ<P, N, VB, 0>::PBA + (int)sizeof(P) <= 128) return f.template operator()<P, N, VB, 128>();
             else return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
@@ -840,89 +607,94 @@ static inline uint32_t stage_bytes_for(uint32_t flags) {
     return (flags & FMX_HINT_LONG_PATTERNS) ? (uint32_t)kStageBytesLong : (uint32_t)kStageBytes;
 }
 
+// The search variant for an index and a launch's staging size: the faithful
+// kernels when no derived structure is loaded; else the derived ones, with
+// the vectorised tail compare for long patterns (56 KB staging).
+static inline int search_var(const QueryArgs &qa, uint32_t sb) {
+    const bool derived = qa.dlut != nullptr || qa.safull != nullptr || qa.text != nullptr || qa.ctx_len != 0;
+    if (!derived) return kVarFaithful;
+    return sb > (uint32_t)kStageBytes ? kVarDerivedLong : kVarDerived;
+}
+
 hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
-                        uint32_t flags, void *d_counts, hipStream_t stream) {
+                        uint32_t flags, void *d_counts, uint32_t *status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    QueryArgs qa = ix->qa;
+    qa.status = status;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
-        const uint32_t sb = stage_bytes_for(flags);
-        if (sb > (uint32_t)kStageBytes)  // long patterns: the vectorised tail compare
-            hipLaunchKernelGGL((k_count<P, N, VB, R, true>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
-                               d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
-        else
-            hipLaunchKernelGGL((k_count<P, N, VB, R, false>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
-                               d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
+        const uint32_t sb = stage_bytes_for(flags), lds = sb + qa.kt_lds_bytes;
+        switch (search_var(qa, sb)) {
+            case kVarFaithful:
+                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarFaithful>), dim3(grid_for(n)), dim3(256), lds, stream,
+                                   qa, d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
+                break;
+            case kVarDerived:
+                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerived>), dim3(grid_for(n)), dim3(256), lds, stream,
+                                   qa, d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
+                break;
+            default:
+                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerivedLong>), dim3(grid_for(n)), dim3(256), lds,
+                                   stream, qa, d_bytes, d_offsets, n, flags, (P *)d_counts, sb);
+        }
         return hipGetLastError();
     });
 }
 
-// The three kernels of a (grouped) split locate, one after another on `stream`.
+// The kernels of a (grouped) locate, one after another on `stream`.
 template <typename P, int N, int VB, int R>
-static hipError_t launch_split(const fmx_index *ix, const LocateGroup &grp, uint32_t tiles, uint32_t sb,
+static hipError_t launch_split(const QueryArgs &qa, const LocateGroup &grp, uint32_t tiles, uint32_t sb,
                                hipStream_t stream) {
-    if (sb > (uint32_t)kStageBytes)
-        hipLaunchKernelGGL((k_search<P, N, VB, R, true>), dim3(tiles), dim3(256), sb, stream, ix->qa, grp, sb);
-    else if (ix->tile_pairs && ix->qa.dlut != nullptr)
-        hipLaunchKernelGGL((k_search2<P, N, VB, R>), dim3((tiles + 1) / 2), dim3(256), 2 * sb, stream, ix->qa, grp,
-                           sb, tiles);
-    else
-        hipLaunchKernelGGL((k_search<P, N, VB, R, false>), dim3(tiles), dim3(256), sb, stream, ix->qa, grp, sb);
+    const uint32_t lds = sb + qa.kt_lds_bytes;
+    switch (search_var(qa, sb)) {
+        case kVarFaithful:
+            hipLaunchKernelGGL((k_search<P, N, VB, R, kVarFaithful>), dim3(tiles), dim3(256), lds, stream, qa, grp,
+                               sb);
+            break;
+        case kVarDerived:
+            hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerived>), dim3(tiles), dim3(256), lds, stream, qa, grp,
+                               sb);
+            break;
+        default:
+            hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerivedLong>), dim3(tiles), dim3(256), lds, stream, qa,
+                               grp, sb);
+    }
     uint32_t fold = 1;
     for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
     if (!fold) hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
-    hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(tiles), dim3(256), 0, stream, ix->qa, grp, fold);
+    hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(tiles), dim3(256), 0, stream, qa, grp, fold);
     return hipGetLastError();
 }
 
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
                          uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs, uint64_t cap,
-                         uint64_t *d_needed, uint32_t *d_ctl, uint64_t *d_tiles, uint64_t tiles_cap,
-                         uint32_t epoch, hipStream_t stream) {
+                         uint64_t *d_needed, uint64_t *d_tiles, uint64_t tiles_cap, uint32_t *status,
+                         hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    QueryArgs qa = ix->qa;
+    qa.status = status;
     if ((n + 255) / 256 > tiles_cap || tiles_cap > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    if (ix->locate_fused && (epoch == 0 || epoch > kLocateEpochs)) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
-        const uint32_t sb = stage_bytes_for(flags);
-        if (ix->locate_fused) {
-            LocateGroup grp{};
-            grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles,
-                                   epoch, (flags & FMX_PATTERN_REVERSED) ? 1u : 0u, flags >> 16};
-            grp.n = 1;
-            if (sb > (uint32_t)kStageBytes)
-                hipLaunchKernelGGL((k_locate<P, N, VB, R, true>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
-                                   grp, sb);
-            else
-                hipLaunchKernelGGL((k_locate<P, N, VB, R, false>), dim3(grid_for(n)), dim3(256), sb, stream, ix->qa,
-                                   grp, sb);
-            return hipGetLastError();
-        }
         LocateGroup grp{};
-        grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles, 1u,
+        grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles,
                                (flags & FMX_PATTERN_REVERSED) ? 1u : 0u, flags >> 16};
         grp.n = 1;
-        return launch_split<P, N, VB, R>(ix, grp, (uint32_t)((n + 255) / 256), sb, stream);
+        return launch_split<P, N, VB, R>(qa, grp, (uint32_t)((n + 255) / 256), stage_bytes_for(flags), stream);
     });
 }
 
 hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
-                               hipStream_t stream) {
+                               uint32_t *status, hipStream_t stream) {
+    QueryArgs qa = ix->qa;
+    qa.status = status;
     if (grp.n == 0 || grp.n > kMaxGroup || grp.tile_begin[0] != 0) return hipErrorInvalidValue;
     uint64_t tiles = 0;
     for (uint32_t j = 0; j < grp.n; ++j) {
         if (grp.b[j].npat == 0 || grp.tile_begin[j] != tiles) return hipErrorInvalidValue;
-        if (ix->locate_fused && (grp.b[j].epoch == 0 || grp.b[j].epoch > kLocateEpochs)) return hipErrorInvalidValue;
         tiles += (grp.b[j].npat + 255) / 256;
     }
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
     return dispatch(ix, [&]<typename P, int N, int VB, int R>() {
-        const uint32_t sb = stage_bytes_for(stage_flags);
-        if (!ix->locate_fused) return launch_split<P, N, VB, R>(ix, grp, (uint32_t)tiles, sb, stream);
-        if (sb > (uint32_t)kStageBytes)  // long patterns: the vectorised tail compare
-            hipLaunchKernelGGL((k_locate<P, N, VB, R, true>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa,
-                               grp, sb);
-        else
-            hipLaunchKernelGGL((k_locate<P, N, VB, R, false>), dim3((unsigned)tiles), dim3(256), sb, stream, ix->qa,
-                               grp, sb);
-        return hipGetLastError();
+        return launch_split<P, N, VB, R>(qa, grp, (uint32_t)tiles, stage_bytes_for(stage_flags), stream);
     });
 }
 
@@ -1044,9 +816,3 @@ hipError_t launch_relayout(fmx_index *ix, hipStream_t stream) {
 
 }  // namespace fmx
 
-#ifdef FMX_PHASE_STAMPS
-extern "C" int fmx_debug_stamps(uint64_t *out, uint64_t n) {
-    if (n > (uint64_t)fmx::kStampWaves * fmx::kStampSlots) n = (uint64_t)fmx::kStampWaves * fmx::kStampSlots;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fmx::g_stamps), n * 8) == hipSuccess ? 0 : 8;
-}
-#endif

@@ -47,16 +47,16 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
     memcpy(t.enc, ox.enc, 256);
     for (uint32_t c = 0; c <= ox.sigma; ++c) t.C[c] = (P)ox.count_array[c];
     for (uint32_t i = 0; i < ox.k && i < (uint32_t)kMaxK; ++i) t.mult[i] = ox.mult[i];
+    t.kt = reinterpret_cast<const P *>(a.kmer);  // (the kernels' LDS copy holds the same entries)
 
     // interleaved records (k_relayout)
     std::vector<uint8_t> occ;
     if constexpr (REC != 0) {
         constexpr int PB = N * VB / 8;
         occ.assign(ox.blocks_len * REC + 16, 0);
-        for (uint64_t q = 0; q < ox.blocks_len; ++q) {
-            memcpy(&occ[q * REC], a.ckpt + q * ox.sigma * sizeof(P), ox.sigma * sizeof(P));
-            memcpy(&occ[q * REC + REC - PB], a.blocks + q * PB, PB);
-        }
+        for (uint64_t q = 0; q < ox.blocks_len; ++q)
+            write_record<P, N, VB, REC>(&occ[q * REC], a.blocks + q * PB, a.ckpt + q * ox.sigma * sizeof(P),
+                                        ox.sigma);
         a.occ = occ.data();
     }
     using O = Occ<P, N, VB, REC>;
@@ -179,10 +179,17 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
             pv.sym = staged.data();
         }
         // option bit 128: the long-pattern kernels' tail compare (LT)
-        const uint32_t bad = long_tails ? search<P, N, VB, REC, true>(a, t, pv, lo, hi, rloc, mask, mode)
-                                        : search<P, N, VB, REC, false>(a, t, pv, lo, hi, rloc, mask, mode);
+        // the variant the engine launches (fmx_query.hip search_var)
+        const bool derived = a.dlut || a.safull || a.text || a.ctx_len;
+        const uint32_t bad = !derived ? search<P, N, VB, REC, kVarFaithful>(a, t, pv, lo, hi, rloc, mask, mode)
+                             : long_tails ? search<P, N, VB, REC, kVarDerivedLong>(a, t, pv, lo, hi, rloc, mask, mode)
+                                          : search<P, N, VB, REC, kVarDerived>(a, t, pv, lo, hi, rloc, mask, mode);
         if (bad) return bad == kStatusEmpty ? ORC_E_EMPTY_PATTERN : ORC_E_SYMBOL;
         const uint64_t cnt = (uint64_t)(hi - lo);
+        if (mode == kHitRows && cnt == 1) {  // k_search settles a single row by its walk
+            rloc = walk_row<P, N, VB, REC>(a, t.C, lo);
+            mode = kHitOne;
+        }
         counts[i] = cnt;
         for (uint64_t j = 0; j < cnt; ++j, ++out) {
             P loc;

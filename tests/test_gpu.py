@@ -506,23 +506,6 @@ def test_large_batch_scan_kernel(pkg, O):
     ix.close()
 
 
-@pytest.mark.parametrize("pb,planes,vb", [(4, 3, 64), (8, 3, 128), (4, 5, 32), (8, 2, 64)])
-def test_fused_locate_kernel(pkg, O, pb, planes, vb, monkeypatch):
-    """FMX_LOCATE_FUSED=1 (the single-kernel k_locate with its look-back):
-    same results as the oracle, for short and long patterns, every load
-    option set; and grouped launches through it."""
-    monkeypatch.setenv("FMX_LOCATE_FUSED", "1")
-    rng = np.random.default_rng(pb * 7 + planes * 3 + vb)
-    chars = rand_chr_list(rng, 4)
-    table = table_from_symbols([bytes([c]) for c in chars])
-    text = rand_text(rng, chars, 30000, 30000)
-    blob = gpu_build(pkg, text, 4, pb, planes, vb, 3, 2, table)
-    pats = [rand_pattern(rng, text, 1, 24) for _ in range(1500)]
-    pats += [rand_pattern(rng, text, 70, 160) for _ in range(300)]  # the long-pattern variant's staging
-    for occ in (1, 4 | 8, 63):
-        check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, reversed_too=(occ == 63))
-
-
 @pytest.mark.parametrize("m", [1, 3, 20, 150, 300])
 def test_fixed_len_hint(pkg, O, m):
     """FMX_HINT_FIXED_LEN: the kernels address each pattern at i * m without
@@ -591,54 +574,4 @@ def test_fixed_len_hint(pkg, O, m):
     with pytest.raises(pkg.FmxError):
         ix.sync()
     ix.sync()  # the status was cleared by the failing sync
-    ix.close()
-
-
-
-def test_tile_pairs(pkg, O, monkeypatch):
-    """FMX_TILE_PAIRS=1 (k_search2: two tiles per workgroup, staged as one
-    span, deep-table reads paired): the oracle's results for variable and
-    fixed lengths, forward and reversed, every load option set with a table;
-    grouped batches with odd tile counts (pairs split across batches run tile
-    by tile)."""
-    import torch
-    monkeypatch.setenv("FMX_TILE_PAIRS", "1")
-    rng = np.random.default_rng(77)
-    chars = rand_chr_list(rng, 4)
-    table = table_from_symbols([bytes([c]) for c in chars])
-    text = rand_text(rng, chars, 40000, 40000)
-    blob = gpu_build(pkg, text, 4, 4, 3, 64, 3, 2, table)
-    pats = [rand_pattern(rng, text, 1, 24) for _ in range(2900)]
-    for occ in (2, 2 | 8 | 32, 63):
-        check_parity(pkg, O, blob, 4, 3, 64, 0, pats, occ, reversed_too=(occ == 63))
-    fixed = [text[s:s + 20] for s in rng.integers(0, len(text) - 20, size=1333)]
-    check_parity(pkg, O, blob, 4, 3, 64, 0, fixed, 63)
-    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
-    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
-    dev = torch.device("cuda:0")
-    bats, jobs = [], []
-    for bi, n in enumerate([300, 700, 1, 256, 513, 1100]):   # 2, 3, 1, 1, 3, 5 tiles
-        rev = bi % 2 == 1
-        ps = [rand_pattern(rng, text, 1, 30) for _ in range(n)]
-        data, offsets = pkg.pack_patterns(ps)
-        want = orc.locate_batch(data, offsets)
-        q = [p[::-1] for p in ps] if rev else ps
-        data, offsets = pkg.pack_patterns(q)
-        cap = int(want[1].size) + 8
-        b = dict(want=want, data=torch.from_numpy(np.concatenate([data, np.zeros(1, np.uint8)])).to(dev),
-                 off=torch.from_numpy(offsets.view(np.int64).copy()).to(dev),
-                 loff=torch.full((n + 1,), -1, dtype=torch.int64, device=dev),
-                 locs=torch.zeros(cap, dtype=torch.int32, device=dev), need=torch.zeros(1, dtype=torch.int64, device=dev))
-        ws = ix.locate_workspace_size(n)
-        b["ws"] = torch.zeros(ws, dtype=torch.uint8, device=dev)
-        jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), n, b["loff"].data_ptr(),
-                                  b["locs"].data_ptr(), cap, b["need"].data_ptr(), b["ws"].data_ptr(), ws,
-                                  reversed=rev, stage_kb=8))
-        bats.append(b)
-    ix.locate_group_async(ix.job_queue(jobs))
-    ix.sync()
-    for b in bats:
-        wo, wl = b["want"]
-        assert np.array_equal(b["loff"].cpu().numpy().view(np.uint64), wo)
-        assert np.array_equal(b["locs"].cpu().numpy()[:wl.size].view(np.uint32), wl)
     ix.close()
