@@ -7,6 +7,7 @@
 // records, deep k-mer table, full SA, text), so the CPU test suite checks the
 // device code paths against the oracle without a GPU.  Blob offsets come from
 // the oracle's parser (oracle/fmx_oracle.c).
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <vector>

@@ -2,7 +2,8 @@
 sharded across ranks, each rank answers its slab against its own replica of
 the index, and the concatenated result must equal the single-process answer.
 The per-rank compute here is the CPU oracle (this tests the sharding and the
-collectives, not the kernels — those are covered by tests/test_gpu.py)."""
+gather bench.py uses — sharding.ShardGather's fixed-size all-gathers and
+device-side assembly — not the kernels, which tests/test_gpu.py covers)."""
 import os
 import socket
 
@@ -43,8 +44,17 @@ def _worker(rank, world, port, result_path):
     s, e = D.shard(len(pats), world, rank)
     sd, so = D.slab_patterns(data, offsets, s, e)
     loff, locs = ix.locate_batch(sd, so)
-    goff, glocs = D.concat_results(torch.from_numpy(loff.astype(np.int64)),
-                                   torch.from_numpy(locs.astype(np.int64)))
+    # the gather bench.py runs: fixed-size slots the results are written into,
+    # two all-gathers, no size exchange
+    cap = torch.tensor([locs.size], dtype=torch.int64)
+    dist.all_reduce(cap, op=dist.ReduceOp.MAX)  # a bound every rank's total stays under
+    sizes = D.shard_sizes(len(pats), world)
+    g = D.SlabGather(world, slots=2, batch=max(sizes), loc_cap=int(cap.item()), count_dtype=torch.int32,
+                     loc_dtype=torch.int32, device="cpu")
+    g.counts_slot(1)[:e - s] = torch.from_numpy(np.diff(loff).astype(np.int32))
+    g.locs_slot(1)[:locs.size] = torch.from_numpy(locs.astype(np.int32))
+    g.gather()
+    goff, glocs = D.concat([g.result(r, 1, sizes[r]) for r in range(world)])
     t = D.max_over_ranks(float(rank + 1))
     if rank == 0:
         ref_off, ref_locs = ix.locate_batch(data, offsets)
@@ -65,8 +75,10 @@ def test_shard_partition(pkg):
             assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
 
 
-def test_two_rank_gloo_concat_matches_single(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_matches_single(tmp_path, world):
+    """world 2 and 3 (ragged shards: 1001 patterns)."""
     import torch.multiprocessing as mp
     out = tmp_path / "res.txt"
-    mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
     assert out.read_text() == "ok"
