@@ -72,8 +72,11 @@ typedef struct fmx_layout {
  * i * m, so the kernels address each pattern's bytes without first reading
  * the offsets (one dependent HBM round trip fewer per workgroup).  The
  * offsets are still read alongside and checked: a batch that disagrees is
- * reported as FMX_E_ARG (its outputs are then undefined).  The host-buffer
- * calls set it themselves when every pattern has the same length. */
+ * reported as FMX_E_ARG (its outputs are then undefined).  Because the bytes
+ * are read before that check, a hint larger than the true length is
+ * undefined behaviour for the reads: the kernels read up to n_patterns * m
+ * bytes from d_bytes, which must be that large.  The host-buffer calls set
+ * the hint themselves when every pattern has the same length. */
 #define FMX_HINT_FIXED_LEN(m) ((((uint32_t)(m)) & 0xffffu) << 16)
 
 /* Load options: device-side structures derived from the blob at load time.
@@ -101,7 +104,14 @@ typedef struct fmx_layout {
                                   interval: such a pattern is settled by that one read (plus a
                                   text compare beyond the packed symbols).  Needs FMX_OPT_DEEP_LUT
                                   and FMX_OPT_TEXT, and n < 2^31 for u32 positions            */
-#define FMX_OPT_DEFAULT (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | \
+/* The default: the blob's own structures, its occ planes and checkpoints
+ * re-laid out as one record per block — the reference's index and algorithm
+ * (FmIndex::load is a zero-copy view, load_from_blob.rs:28-85; this is one
+ * device copy plus a 1/2.7 size re-layout, milliseconds at 1 Gbp). */
+#define FMX_OPT_DEFAULT FMX_OCC_INTERLEAVED
+/* Every derived structure: ~55x the blob's HBM at C2 (147 GB) and seconds of
+ * load time, paid back only after ~10^10 patterns (bench.py "derived"). */
+#define FMX_OPT_DERIVED (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | \
                          FMX_OPT_ROW_CONTEXT | FMX_OPT_LUT_ROWS)
 
 typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
@@ -141,13 +151,14 @@ int fmx_device_count(void);
  * consistency checks the reference leaves to the type system, then copies the
  * blob to HBM of `device` once.  The host blob is borrowed for fmx_blob() only.
  * On FMX_E_SIZE, *expected_total / *actual_total receive the two sizes.
- * options: FMX_OCC_* | FMX_OPT_* (FMX_OPT_DEFAULT recommended). */
+ * options: FMX_OCC_* | FMX_OPT_* (FMX_OPT_DEFAULT: the blob's own structures). */
 fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, int device,
                     uint32_t options, fmx_index **out, uint64_t *expected_total,
                     uint64_t *actual_total);
 
 /* Same, for a blob already resident in HBM of `device` (e.g. written by
- * fmx_build_device).  The device blob is borrowed and must outlive the index. */
+ * fmx_build_device).  The device blob is borrowed and must outlive the index.
+ * Starts after all work already queued on the device (it synchronises). */
 fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout layout, int device,
                            uint32_t options, fmx_index **out, uint64_t *expected_total,
                            uint64_t *actual_total);
@@ -263,7 +274,9 @@ fmx_status fmx_build_blob_size(uint64_t text_len, uint32_t symbol_count, fmx_lay
                                uint32_t kmer_size, uint32_t sampling_ratio, uint64_t *out_size);
 
 /* d_text and d_blob are device buffers on `device`; d_blob must be 16-B aligned
- * and exactly fmx_build_blob_size bytes.  Synchronous. */
+ * and exactly fmx_build_blob_size bytes.  Synchronous: starts after all work
+ * already queued on the device (whichever stream wrote d_text) and returns
+ * when the blob is complete. */
 fmx_status fmx_build_device(const uint8_t *d_text, uint64_t text_len, const uint8_t *table,
                             uint32_t symbol_count, fmx_layout layout, uint32_t kmer_size,
                             uint32_t sampling_ratio, uint8_t *d_blob, uint64_t blob_len, int device);

@@ -356,11 +356,14 @@ class FmIndex:
     @classmethod
     def load(cls, blob, position: Position = u32, block: Optional[_Block] = None,
              text_encoder=text_encoders.EncodingTable, device: int = 0,
-             occ: str = "interleaved", deep_lut: bool = True, full_sa: bool = True, text: bool = True,
-             context: bool = True, lut_rows: bool = True, options: Optional[int] = None) -> "FmIndex":
+             occ: str = "interleaved", deep_lut: bool = False, full_sa: bool = False, text: bool = False,
+             context: bool = False, lut_rows: bool = False, options: Optional[int] = None) -> "FmIndex":
         """``FmIndex::load`` (load_from_blob.rs:28-85): validate, then copy the
-        blob to HBM once and derive the device structures chosen by the flags
-        (results are identical with any of them):
+        blob to HBM once.  By default the index is the reference's own: the
+        blob, its occ planes and checkpoints re-laid out as one record per
+        block (FMX_OPT_DEFAULT).  The flags add derived device structures
+        (results are identical with any of them; they cost HBM — ~55x the
+        blob at C2 with all of them — and load time; bench.py "derived"):
         `occ` — "blob" reads the blob's arrays as they are, "interleaved"
         re-lays checkpoint + planes into one HBM line per block; `deep_lut` —
         the device K-mer interval table (FMX_OPT_DEEP_LUT); `full_sa` — the
@@ -368,7 +371,8 @@ class FmIndex:
         single-row tail verification (FMX_OPT_TEXT); `context` — row records
         {SA, preceding symbols} so that small intervals finish with one scan
         (FMX_OPT_ROW_CONTEXT); `lut_rows` — single-row deep-table entries
-        that hold the row's location (FMX_OPT_LUT_ROWS).  `options` overrides all."""
+        that hold the row's location (FMX_OPT_LUT_ROWS).  `options` overrides all
+        (FMX_OPT_DERIVED: every derived structure)."""
         block = block or blocks.Block2(Vector.U64)
         if isinstance(text_encoder, type):
             text_encoder = text_encoder.__new__(text_encoder)
@@ -394,8 +398,8 @@ class FmIndex:
     @classmethod
     def load_device(cls, d_blob: int, blob_len: int, position: Position = u32,
                     block: Optional[_Block] = None, text_encoder=text_encoders.EncodingTable,
-                    device: int = 0, occ: str = "interleaved", deep_lut: bool = True, full_sa: bool = True,
-                    text: bool = True, context: bool = True, lut_rows: bool = True,
+                    device: int = 0, occ: str = "interleaved", deep_lut: bool = False, full_sa: bool = False,
+                    text: bool = False, context: bool = False, lut_rows: bool = False,
                     options: Optional[int] = None) -> "FmIndex":
         """Load a blob already resident in HBM (borrowed, must outlive the index)."""
         block = block or blocks.Block2(Vector.U64)
@@ -416,8 +420,8 @@ class FmIndex:
     @classmethod
     def load_file(cls, path, position: Position = u32, block: Optional[_Block] = None,
                   text_encoder=text_encoders.EncodingTable, device: int = 0, occ: str = "interleaved",
-                  deep_lut: bool = True, full_sa: bool = True, text: bool = True, context: bool = True,
-                  lut_rows: bool = True, options: Optional[int] = None, chunk_bytes: int = 0) -> "FmIndex":
+                  deep_lut: bool = False, full_sa: bool = False, text: bool = False, context: bool = False,
+                  lut_rows: bool = False, options: Optional[int] = None, chunk_bytes: int = 0) -> "FmIndex":
         """Blob file -> HBM (fmx_load_file): what the bench's mmap loader
         (bench/src/locate/sview_mmap.rs:17-45) followed by ``FmIndex::load``
         does, as a streamed ingest — the header is validated from the file,

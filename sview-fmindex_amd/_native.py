@@ -35,7 +35,8 @@ FMX_OPT_FULL_SA = 4
 FMX_OPT_TEXT = 8
 FMX_OPT_ROW_CONTEXT = 16
 FMX_OPT_LUT_ROWS = 32
-FMX_OPT_DEFAULT = (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | FMX_OPT_ROW_CONTEXT
+FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED
+FMX_OPT_DERIVED = (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | FMX_OPT_ROW_CONTEXT
                    | FMX_OPT_LUT_ROWS)
 
 

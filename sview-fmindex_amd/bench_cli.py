@@ -155,7 +155,7 @@ def format_results(loc_offsets: np.ndarray, locs: np.ndarray) -> bytes:
 
 
 def locate(data_dir: str, algorithm: str, treat_t_as_wildcard: bool, drop_caches: bool = False,
-           batch: int = 1 << 20, device: int = 0):
+           batch: int = 1 << 20, device: int = 0, options=None):
     pkg = _pkg()
     pattern_path = os.path.join(data_dir, "pattern.txt")
     if not os.path.exists(pattern_path):
@@ -175,12 +175,14 @@ def locate(data_dir: str, algorithm: str, treat_t_as_wildcard: bool, drop_caches
         print(f"Using blob file: {blob_path}")
         t0 = time.perf_counter_ns()
         if a == "sview-mmap":
-            ix = pkg.FmIndex.load_file(blob_path, pkg.u32, block, pkg.text_encoders.EncodingTable, device=device)
+            ix = pkg.FmIndex.load_file(blob_path, pkg.u32, block, pkg.text_encoders.EncodingTable, device=device,
+                                       options=options)
         else:
             blob = pkg.aligned_buffer(os.path.getsize(blob_path))
             with open(blob_path, "rb") as f:
                 f.readinto(memoryview(blob))
-            ix = pkg.FmIndex.load(blob, pkg.u32, block, pkg.text_encoders.EncodingTable, device=device)
+            ix = pkg.FmIndex.load(blob, pkg.u32, block, pkg.text_encoders.EncodingTable, device=device,
+                                  options=options)
         load_ns = time.perf_counter_ns() - t0
         t0 = time.perf_counter_ns()
         pats = read_patterns(pattern_path)
@@ -234,6 +236,8 @@ def main(argv=None):
     lo.add_argument("--drop-caches", action="store_true")
     lo.add_argument("--batch", type=int, default=1 << 20, help="patterns per fmx_locate_batch call")
     lo.add_argument("--device", type=int, default=0)
+    lo.add_argument("--options", type=int, default=None,
+                    help="fmx_load options (default FMX_OPT_DEFAULT: the blob's own structures)")
     a = ap.parse_args(argv)
     t0 = time.perf_counter_ns()
     if a.command == "generate":
@@ -246,7 +250,7 @@ def main(argv=None):
     elif a.command == "build":
         build(a.data_dir, a.algorithm, a.sasr, a.klts, a.treat_t_as_wildcard, a.device)
     elif a.command == "locate":
-        locate(a.data_dir, a.algorithm, a.treat_t_as_wildcard, a.drop_caches, a.batch, a.device)
+        locate(a.data_dir, a.algorithm, a.treat_t_as_wildcard, a.drop_caches, a.batch, a.device, a.options)
     print(f"Total time: {time.perf_counter_ns() - t0} ns")
 
 

@@ -461,6 +461,7 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
     if (((uintptr_t)d_blob) % align_of(layout) != 0) return FMX_E_ALIGN;
     DeviceGuard dg(device);
     if (!dg.ok) return FMX_E_DEVICE;
+    if (hipDeviceSynchronize() != hipSuccess) return FMX_E_DEVICE;  // the blob's writers, on any stream
     BlobView bv;
     BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
         if (off + len > blob_len) return false;
@@ -908,6 +909,9 @@ fmx_status fmx_build_device(const uint8_t *d_text, uint64_t text_len, const uint
     if (!d_blob || (text_len && !d_text)) return FMX_E_ARG;
     DeviceGuard dg(device);
     if (!dg.ok) return FMX_E_DEVICE;
+    // d_text may still be being written by work queued on any stream of the
+    // device (the caller's): this synchronous call starts after all of it
+    if (hipDeviceSynchronize() != hipSuccess) return FMX_E_DEVICE;
     hipStream_t s;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
     fmx_status st = build_device(d_text, text_len, table, symbol_count, layout, kmer_size, sampling_ratio, d_blob,

@@ -176,6 +176,28 @@ struct LocateGroup {
 };
 hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
                                uint32_t *status, hipStream_t stream);
+// k_emit sums the earlier tiles' counts itself for batches of at most this
+// many tiles; larger ones get their tile offsets from k_scan first.
+constexpr uint64_t kFoldTiles = 2048;
+
+// The kernels that depend on the occ layout, one table per (P, N) pair
+// (fmx_layout.hip, one translation unit per pair); vb = V bits, rec = 0
+// (blob layout) or the interleaved record bytes, var = search variant
+// (kVarFaithful / kVarDerived / kVarDerivedLong, fmx_device.hpp).
+struct LayoutOps {
+    hipError_t (*count)(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const uint8_t *bytes,
+                        const uint64_t *offs, uint64_t n, uint32_t flags, void *counts, uint32_t sb, hipStream_t s);
+    hipError_t (*search)(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const LocateGroup &grp,
+                         uint32_t tiles, uint32_t sb, hipStream_t s);
+    hipError_t (*emit)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp, uint32_t tiles,
+                       uint32_t fold, hipStream_t s);
+    hipError_t (*dlut_level)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
+                             void *child, hipStream_t s);
+    hipError_t (*full_sa)(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t n, void *sa_out,
+                          uint32_t stride, hipStream_t s);
+    hipError_t (*relayout)(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t blocks_len, uint8_t *occ,
+                           hipStream_t s);
+};
 uint64_t locate_tiles_cap(uint64_t n);
 // Bytes per pattern of the search-result records in the locate workspace.
 uint64_t locate_rec_bytes(uint32_t pos_bytes);

@@ -1,0 +1,459 @@
+// fmx_kernels.hpp — the query kernels that depend on the occ layout (P, N,
+// V, record size): k_count, k_search, k_emit, the deep-table level step, the
+// full-SA walk and the record re-layout.  Instantiated per (P, N) in its own
+// translation unit (fmx_layout.hip, one object per layout, built in
+// parallel); launched through the LayoutOps table (fmx_internal.hpp).
+// Search/walk arithmetic: fmx_device.hpp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "fmx_device.hpp"
+#include "fmx_internal.hpp"
+
+namespace fmx {
+
+static inline unsigned grid_for(uint64_t threads) { return (unsigned)((threads + 255) / 256); }
+// k_dlut_level: one thread per parent up to 2^24 workgroups, then grid-stride
+static inline unsigned grid_dlut(uint64_t np) {
+    const uint64_t g = (np + 255) / 256;
+    return (unsigned)(g < (1ull << 24) ? (g ? g : 1) : (1ull << 24) - 1);
+}
+static inline unsigned grid_stride_for(uint64_t n) {
+    const uint64_t g = (n + 255) / 256;
+    return (unsigned)(g < 65536 ? (g ? g : 1) : 65536);
+}
+
+// The per-workgroup tables: encoding table, C array, k-mer multipliers, and
+// — when it is small (QueryArgs::kt_lds_bytes) — the blob's k-mer count
+// table, copied into LDS at `kt_lds` so that the seed's two reads are LDS
+// reads.  Visible after the caller's next barrier.
+template <typename P>
+__device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s, uint8_t *kt_lds) {
+    const int t = threadIdx.x;
+    s.enc[t] = a.enc[t];
+    if (t < kMaxSigma) s.dig[t] = a.dlut_dig[t];
+    if ((uint32_t)t <= a.sigma) s.C[t] = (P)a.C[t];
+    if ((uint32_t)t < a.k) s.mult[t] = a.mult[t];
+    if (a.kt_lds_bytes && kt_lds) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(a.kmer);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(kt_lds);
+        for (uint32_t i = t; i < a.kt_lds_bytes / 4; i += 256) dst[i] = src[i];
+        if (t == 0) s.kt = reinterpret_cast<const P *>(kt_lds);
+    } else if (t == 0) {
+        s.kt = reinterpret_cast<const P *>(a.kmer);
+    }
+}
+
+// 256-thread workgroup exclusive scan of one u64 per thread.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total, uint64_t *sh /*[4]*/) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (i < w) before += sh[i];
+        all += sh[i];
+    }
+    __syncthreads();
+    *total = all;
+    return before + x - v;
+}
+
+// ----------------------------------------------------------------- k_count
+
+// Stage the workgroup's patterns [first, first+256) as encoded symbols in
+// LDS (pattern order; a reversed input range is stored reversed, which puts
+// every pattern back in pattern order).  One round trip for the offsets (each
+// thread its own pattern's bounds, plus the tile's), one for the bytes: 16-B
+// aligned vectors, up to four per thread in flight (an aligned vector holding
+// at least one byte of the batch never leaves the batch's page).  Returns
+// false if the tile does not fit; the patterns are then read from HBM.
+// NP patterns per thread (a pair of tiles: NP = 2): thread t stages and
+// later searches patterns first + t, first + 256 + t, ... of one span.
+template <typename P, int NP>
+__device__ __forceinline__ bool stage_span(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
+                                           const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
+                                           uint32_t stage_bytes, uint32_t stride, uint32_t *status,
+                                           uint64_t *beg, uint64_t *end, uint64_t &b0, uint64_t &b1) {
+    const uint64_t last = first + 256 * NP < npat ? first + 256 * NP : npat;
+    uint64_t chk[NP];
+    if (stride) {
+        // FMX_HINT_FIXED_LEN: offs[i] == i * stride, so the byte loads need
+        // not wait for the offsets; each thread's own end offsets are loaded
+        // alongside them and checked once they have arrived.
+        b0 = first * stride;
+        b1 = last * stride;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const uint64_t i = first + 256 * q + threadIdx.x;
+            beg[q] = i < npat ? i * stride : 0;
+            end[q] = i < npat ? beg[q] + stride : 0;
+            chk[q] = i < npat ? offs[i + 1] : 0;
+        }
+        if (first == 0 && threadIdx.x == 0 && offs[0] != 0) atomicOr(status, kStatusStride);
+    } else {
+        b0 = offs[first];
+        b1 = offs[last];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const uint64_t i = first + 256 * q + threadIdx.x;
+            beg[q] = i < npat ? offs[i] : 0;
+            end[q] = i < npat ? offs[i + 1] : 0;
+            chk[q] = end[q];
+        }
+    }
+    const uint64_t len = b1 - b0;
+    uint32_t bad_stride = 0;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) bad_stride |= chk[q] != end[q];
+    // the encoding table (stage_tables, written by every thread) is read below
+    __syncthreads();
+    if (len > stage_bytes) {
+        if (bad_stride) atomicOr(status, kStatusStride);
+        return false;
+    }
+    using V4 = uint32_t __attribute__((ext_vector_type(4)));
+    const uint64_t a0 = b0 & ~15ull;
+    const uint32_t nv = (uint32_t)((b1 - a0 + 15) >> 4);
+    const V4 *src = reinterpret_cast<const V4 *>(bytes + a0);
+    // 32-bit positions within the span (len <= stage_bytes): byte w of
+    // vector v is span byte 16 v + w - lead, kept if below len (unsigned)
+    const uint32_t lead = (uint32_t)(b0 - a0), len32 = (uint32_t)len;
+    for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 256) {
+        V4 x[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t v = v0 + u * 256 + threadIdx.x;
+            if (v < nv) x[u] = src[v];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t v = v0 + u * 256 + threadIdx.x;
+            if (v >= nv) continue;
+            const uint32_t base = 16u * v - lead;
+#pragma unroll
+            for (uint32_t w = 0; w < 16; ++w) {
+                const uint32_t x0 = base + w;
+                if (x0 < len32)
+                    s_pat[rev ? len32 - 1u - x0 : x0] = s.enc[(x[u][w >> 2] >> (8 * (w & 3))) & 0xffu];
+            }
+        }
+    }
+    if (bad_stride) atomicOr(status, kStatusStride);
+    return true;
+}
+
+template <typename P>
+__device__ __forceinline__ bool stage_patterns(const Tables<P> &s, uint8_t *s_pat, const uint8_t *bytes,
+                                               const uint64_t *offs, uint64_t npat, uint64_t first, bool rev,
+                                               uint32_t stage_bytes, uint32_t stride, uint32_t *status,
+                                               uint64_t &beg, uint64_t &end, uint64_t &b0, uint64_t &b1) {
+    return stage_span<P, 1>(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, stride, status, &beg, &end, b0,
+                            b1);
+}
+
+template <typename P>
+__device__ __forceinline__ PatView pattern_view(const Tables<P> &s, const uint8_t *s_pat, bool staged,
+                                                const uint8_t *bytes, uint64_t beg, uint64_t end, uint64_t b0,
+                                                uint64_t b1, bool rev) {
+    PatView pv;
+    pv.m = end - beg;
+    pv.rev = rev;
+    pv.raw = bytes + beg;
+    pv.enc = s.enc;
+    pv.sym = staged ? s_pat + (rev ? b1 - end : beg - b0) : nullptr;
+    return pv;
+}
+
+template <typename P, int N, int VB, int REC, int VAR>
+__global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t *__restrict__ bytes,
+                                               const uint64_t *__restrict__ offs, uint64_t npat,
+                                               uint32_t flags, P *__restrict__ out_cnt, uint32_t stage_bytes) {
+    __shared__ Tables<P> s;
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    stage_tables(a, s, s_pat + stage_bytes);
+    __syncthreads();
+    const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
+    const uint64_t first = (uint64_t)blockIdx.x * 256u;
+    uint64_t beg, end, b0, b1;
+    const bool staged = stage_patterns(s, s_pat, bytes, offs, npat, first, rev, stage_bytes, flags >> 16, a.status, beg,
+                                       end, b0, b1);
+    __syncthreads();
+    const uint64_t i = first + threadIdx.x;
+    if (i >= npat) return;
+    const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
+    P lo, hi, rloc;
+    uint64_t mask;
+    uint32_t mode;
+    const uint32_t bad = search<P, N, VB, REC, VAR>(a, s, pv, lo, hi, rloc, mask, mode);
+    if (bad) atomicOr(a.status, bad);
+    out_cnt[i] = hi - lo;
+}
+
+// ------------------------------------------------------------ locations
+
+// The locations of a wave's 64 patterns (lane j: pattern with output slots
+// [my_off, my_off + cnt) and its search result), every occurrence row dealt
+// to the next free lane so that skewed counts keep the wave busy
+// (write_locations_to_buffer, src/locate/mod.rs:14-37): lane t of a round
+// finds its pattern by a binary search over the lanes' first slots.
+template <typename P, int N, int VB, int REC>
+__device__ __forceinline__ void emit_locations(const QueryArgs &a, const P *C, uint64_t my_off, uint64_t cnt, P lo,
+                                               P rloc, uint64_t mask, uint32_t mode, uint64_t cap,
+                                               P *__restrict__ out_locs) {
+    // settled wave (every pattern of a large text, k_search walked its row):
+    // each lane writes its own location, no dealing
+    if (__all(mode == kHitOne)) {
+        if (cnt == 1 && my_off < cap) out_locs[my_off] = rloc;
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    const uint64_t w_start = __shfl(my_off, 0);
+    const uint64_t w_end = __shfl(my_off + cnt, 63);
+    for (uint64_t t0 = w_start; t0 < w_end; t0 += 64) {
+        const uint64_t t = t0 + lane;
+        int jl = 0;  // largest lane whose first slot is <= t
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint64_t o = __shfl(my_off, jl + step);
+            if (o <= t) jl += step;
+        }
+        const P lo_j = __shfl(lo, jl);
+        const uint64_t off_j = __shfl(my_off, jl);
+        const P rloc_j = __shfl(rloc, jl);
+        const uint32_t mode_j = (uint32_t)__shfl((int)mode, jl);
+        const uint64_t mask_j = __shfl(mask, jl);
+        if (t < w_end) {
+            const uint64_t q = t - off_j;  // occurrence q of pattern jl
+            P loc;
+            if (mode_j == kHitOne) {
+                loc = rloc_j;  // resolved against the text: its one location
+            } else if (mode_j == kHitMask) {
+                uint64_t mk = mask_j;  // the q-th matching row of a scanned interval
+                for (uint64_t u = 0; u < q; ++u) mk &= mk - 1;
+                const P row = lo_j + (P)__builtin_ctzll(mk);
+                loc = reinterpret_cast<const P *>(a.safull)[(uint64_t)row * a.sa_stride] - rloc_j;
+            } else {
+                loc = walk_row<P, N, VB, REC>(a, C, lo_j + (P)q);
+            }
+            if (t < cap) out_locs[t] = loc;
+        }
+    }
+}
+
+
+// ------------------------------------------------- k_search + k_emit (split)
+
+// A pattern's search result, handed from k_search to k_emit (P-typed words):
+//   rows (kHitRows): a = lo,   b = count, x = 0
+//   one  (kHitOne):  a = rloc, b = count, x = 1
+//   mask (kHitMask): a = lo,   b = rloc,  x = mask (>= 2 bits set, count = popcount)
+template <typename P>
+struct SearchRec {
+    P a, b;
+    uint64_t x;
+};
+
+template <typename P>
+__device__ __forceinline__ SearchRec<P> pack_rec(P lo, P hi, P rloc, uint64_t mask, uint32_t mode) {
+    if (mode == kHitOne) return {rloc, (P)(hi - lo), 1ull};
+    if (mode == kHitMask) return {lo, rloc, mask};
+    return {lo, (P)(hi - lo), 0ull};
+}
+
+template <typename P>
+__device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &rloc, uint64_t &mask,
+                                               uint32_t &mode) {
+    // Selects, not branches: the if-chain form of this decode was miscompiled
+    // (hipcc 7.2, gfx950: lo/rloc left undefined on the x > 1 path).
+    const uint64_t x = r.x;
+    const bool is_one = x == 1, is_mask = x > 1;
+    mode = is_mask ? kHitMask : (is_one ? kHitOne : kHitRows);
+    lo = is_one ? P(0) : r.a;
+    rloc = is_mask ? r.b : (is_one ? r.a : P(0));
+    mask = is_mask ? x : 0ull;
+    return is_mask ? (uint64_t)__builtin_popcountll(x) : (uint64_t)r.b;
+}
+
+// The locate launch: k_search, (k_scan,) k_emit.
+// No workgroup ever waits on another, so nothing depends on the order or
+// placement in which workgroups are dispatched (MI355X_MICROARCH.md: HIP
+// promises neither; a look-back that assumes in-order dispatch can deadlock
+// when launches on several streams share the CUs).  Per batch of a group:
+// workspace = [256 B][tile counts: G][tile offsets: G][search records: n].
+
+// This workgroup's batch of a grouped launch (workgroup-uniform).
+__device__ __forceinline__ uint32_t group_batch(const LocateGroup &grp, uint32_t vt) {
+    uint32_t jb = 0;
+#pragma unroll
+    for (uint32_t t = 1; t < kMaxGroup; ++t)
+        if (t < grp.n && vt >= grp.tile_begin[t]) jb = t;
+    return jb;
+}
+
+// 1. Search every pattern; its result record, its count; the tile's count.
+template <typename P, int N, int VB, int REC, int VAR>
+__device__ __forceinline__ void search_tile(const QueryArgs &a, const LocateGroup &grp, const Tables<P> &s,
+                                            uint8_t *s_pat, uint64_t *s_scan, uint32_t stage_bytes, uint32_t vt) {
+    const uint32_t jb = group_batch(grp, vt);
+    const LocateBatch &B = grp.b[jb];
+    const uint8_t *__restrict__ bytes = B.bytes;
+    const uint64_t *__restrict__ offs = B.offs;
+    const uint64_t npat = B.npat;
+    const bool rev = B.rev != 0;
+    const uint32_t g = vt - grp.tile_begin[jb];
+    const uint64_t G = (npat + 255) / 256;
+    SearchRec<P> *__restrict__ recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
+    uint64_t beg, end, b0, b1;
+    const bool staged =
+        stage_patterns(s, s_pat, bytes, offs, npat, (uint64_t)g * 256u, rev, stage_bytes, B.stride, a.status,
+                       beg, end, b0, b1);
+    __syncthreads();
+    const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
+    uint64_t cnt = 0;
+    if (i < npat) {
+        const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
+        P lo, hi, rloc;
+        uint64_t mask;
+        uint32_t mode;
+        const uint32_t bad = search<P, N, VB, REC, VAR>(a, s, pv, lo, hi, rloc, mask, mode);
+        if (bad) atomicOr(a.status, bad);
+        cnt = (uint64_t)(hi - lo);
+        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = hi - lo;
+        // one row (most patterns of a large text): its location now, while
+        // this lane's chain is live (locate/mod.rs:19-35); k_emit then only
+        // copies it
+        if (mode == kHitRows && cnt == 1) {
+            rloc = walk_row<P, N, VB, REC>(a, s.C, lo);
+            mode = kHitOne;
+        }
+        recs[i] = pack_rec<P>(lo, hi, rloc, mask, mode);
+    }
+    uint64_t agg;
+    block_excl_scan(cnt, &agg, s_scan);  // (its barriers end every read of s_pat)
+    if (threadIdx.x == 0) B.tiles[g] = agg;
+}
+
+template <typename P, int N, int VB, int REC, int VAR>
+__global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
+                                                             uint32_t stage_bytes) {
+    __shared__ Tables<P> s;
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    __shared__ uint64_t s_scan[4];
+    stage_tables(a, s, s_pat + stage_bytes);
+    search_tile<P, N, VB, REC, VAR>(a, grp, s, s_pat, s_scan, stage_bytes, blockIdx.x);
+}
+
+// 3. Output offsets (tile offset + in-tile scan) and every location, rows
+// dealt across each wave's lanes (emit_locations).
+// fold: batches of at most kFoldTiles tiles need no k_scan: each workgroup
+// sums the counts of the tiles before its own (all final: k_search is done),
+// and the last tile writes the batch total.
+
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGroup grp, uint32_t fold) {
+    __shared__ P sC[kMaxSigma + 1];
+    __shared__ uint64_t s_scan[4], s_part[4];
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
+    const uint32_t jb = group_batch(grp, blockIdx.x);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t npat = B.npat, G = (npat + 255) / 256;
+    const uint64_t g = blockIdx.x - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
+    const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
+    P lo = 0, rloc = 0;
+    uint64_t mask = 0, cnt = 0;
+    uint32_t mode = kHitOne;
+    if (i < npat) cnt = unpack_rec<P>(recs[i], lo, rloc, mask, mode);
+    // the tile's base offset (fold: the earlier tiles' counts, summed here)
+    // and the exclusive scan of the counts, one barrier for both
+    uint64_t part = 0;
+    if (fold)
+        for (uint64_t t = threadIdx.x; t < g; t += 256) part += B.tiles[t];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t x = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+        part += __shfl_xor(part, d);
+    }
+    if (lane == 63) { s_scan[wv] = x; s_part[wv] = part; }
+    __syncthreads();  // (also publishes sC)
+    uint64_t before = 0, agg = 0, base = fold ? 0 : B.tiles[G + g];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w < wv) before += s_scan[w];
+        agg += s_scan[w];
+        if (fold) base += s_part[w];
+    }
+    const uint64_t my_off = base + before + x - cnt;
+    if (fold && g == G - 1 && threadIdx.x == 0) {
+        B.loc_off[npat] = base + agg;
+        *B.needed = base + agg;
+    }
+    if (i < npat) B.loc_off[i] = my_off;
+    emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, B.cap,
+                                  reinterpret_cast<P *>(B.out_locs));
+}
+
+// Level j -> j+1: child string cS has code digit(c)*S^j + code(S); its
+// interval is one LF step (next_pos_range, locate/mod.rs:39-45) from S's.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_dlut_level(const QueryArgs a, const P *__restrict__ parent, uint64_t np,
+                                                    P *__restrict__ child) {
+    using O = Occ<P, N, VB, REC>;
+    const P sent = (P)a.sentinel;
+    // grid-stride: a launch covers at most 2^32 - 1 work-items (S^16 parents
+    // for a K = 17 table would not fit one thread each)
+    for (uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x; x < np; x += (uint64_t)gridDim.x * 256u) {
+    const P lo = parent[2 * x], hi = parent[2 * x + 1];
+    for (uint32_t d = 0; d < a.dlut_sigma; ++d) {
+        const uint32_t c = a.dlut_sym[d];
+        P clo = 0, chi = 0;
+        if (lo < hi) {
+            const P pre = (P)a.C[c];
+            clo = pre + O::rank_at(a, lo + (lo < sent ? P(1) : P(0)), c);
+            chi = pre + O::rank_at(a, hi + (hi < sent ? P(1) : P(0)), c);
+        }
+        P *dst = child + 2 * ((uint64_t)d * np + x);
+        dst[0] = clo;
+        dst[1] = chi;
+    }
+    }
+}
+
+// ------------------------------------------------ full SA and text recovery
+
+// SA[r] for every reduced row r: the locate walk of every row
+// (locate/mod.rs:19-35), done once at load.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_full_sa(const QueryArgs a, uint64_t n, P *__restrict__ sa_out,
+                                                 uint32_t stride) {
+    __shared__ Tables<P> s;
+    stage_tables(a, s, nullptr);
+    __syncthreads();
+    QueryArgs b = a;
+    b.safull = nullptr;
+    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256)
+        sa_out[r * stride] = walk_row<P, N, VB, REC>(b, s.C, (P)r);
+}
+
+// -------------------------------------------------------------- k_relayout
+
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_relayout(const QueryArgs a, uint64_t blocks_len, uint8_t *__restrict__ occ) {
+    const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (q >= blocks_len) return;
+    write_record<P, N, VB, REC>(occ + q * REC, a.blocks + q * (N * VB / 8), a.ckpt + q * a.sigma * sizeof(P),
+                                a.sigma);
+}
+
+}  // namespace fmx

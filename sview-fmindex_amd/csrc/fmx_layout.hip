@@ -1,0 +1,134 @@
+// fmx_layout.hip — the layout-dependent kernels of one (P, N) pair: compiled
+// once per pair (-DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6, csrc/Makefile), each
+// object exporting its LayoutOps table layout_ops_<P>_<N>.  Within a pair the
+// vector width V (32/64/128) and the occ record size (blob layout, 64-B or
+// 128-B interleaved records) are dispatched at run time.
+#include "fmx_kernels.hpp"
+
+#if !defined(FMX_LAYOUT_P) || !defined(FMX_LAYOUT_N)
+#error "build with -DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6"
+#endif
+
+namespace fmx {
+namespace {
+
+using P = std::conditional_t<FMX_LAYOUT_P == 4, uint32_t, uint64_t>;
+constexpr int N = FMX_LAYOUT_N;
+
+template <int VB, class F>
+hipError_t disp_rec(uint32_t rec, F &&f) {
+    switch (rec) {
+        case 0: return f.template operator()<VB, 0>();
+        case 64:
+            if constexpr (Occ<P, N, VB, 0>::PBA + (int)sizeof(P) <= 64) return f.template operator()<VB, 64>();
+            else return hipErrorInvalidValue;
+        case 128:
+            if constexpr (Occ<P, N, VB, 0>::PBA + (int)sizeof(P) <= 128) return f.template operator()<VB, 128>();
+            else return hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// f.template operator()<VB, REC>() for the layout's vector width and record size
+template <class F>
+hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
+    switch (vb) {
+        case 32: return disp_rec<32>(rec, f);
+        case 64: return disp_rec<64>(rec, f);
+        case 128: return disp_rec<128>(rec, f);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+[[maybe_unused]] hipError_t op_count(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const uint8_t *bytes,
+                    const uint64_t *offs, uint64_t n, uint32_t flags, void *counts, uint32_t sb, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        const uint32_t lds = sb + qa.kt_lds_bytes;
+        switch (var) {
+            case kVarFaithful:
+                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarFaithful>), dim3(grid_for(n)), dim3(256), lds, s, qa,
+                                   bytes, offs, n, flags, (P *)counts, sb);
+                break;
+            case kVarDerived:
+                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerived>), dim3(grid_for(n)), dim3(256), lds, s, qa,
+                                   bytes, offs, n, flags, (P *)counts, sb);
+                break;
+            default:
+                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerivedLong>), dim3(grid_for(n)), dim3(256), lds, s,
+                                   qa, bytes, offs, n, flags, (P *)counts, sb);
+        }
+        return hipGetLastError();
+    });
+}
+
+[[maybe_unused]] hipError_t op_search(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const LocateGroup &grp,
+                     uint32_t tiles, uint32_t sb, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        const uint32_t lds = sb + qa.kt_lds_bytes;
+        switch (var) {
+            case kVarFaithful:
+                hipLaunchKernelGGL((k_search<P, N, VB, R, kVarFaithful>), dim3(tiles), dim3(256), lds, s, qa, grp,
+                                   sb);
+                break;
+            case kVarDerived:
+                hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerived>), dim3(tiles), dim3(256), lds, s, qa, grp,
+                                   sb);
+                break;
+            default:
+                hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerivedLong>), dim3(tiles), dim3(256), lds, s, qa,
+                                   grp, sb);
+        }
+        return hipGetLastError();
+    });
+}
+
+[[maybe_unused]] hipError_t op_emit(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp, uint32_t tiles,
+                   uint32_t fold, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        hipLaunchKernelGGL((k_emit<P, N, VB, R>), dim3(tiles), dim3(256), 0, s, qa, grp, fold);
+        return hipGetLastError();
+    });
+}
+
+[[maybe_unused]] hipError_t op_dlut_level(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
+                         void *child, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        hipLaunchKernelGGL((k_dlut_level<P, N, VB, R>), dim3(grid_dlut(np)), dim3(256), 0, s, qa,
+                           (const P *)parent, np, (P *)child);
+        return hipGetLastError();
+    });
+}
+
+[[maybe_unused]] hipError_t op_full_sa(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t n, void *sa_out, uint32_t stride,
+                      hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        hipLaunchKernelGGL((k_full_sa<P, N, VB, R>), dim3(grid_stride_for(n)), dim3(256), 0, s, qa, n,
+                           (P *)sa_out, stride);
+        return hipGetLastError();
+    });
+}
+
+[[maybe_unused]] hipError_t op_relayout(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t blocks_len, uint8_t *occ,
+                       hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        if constexpr (R != 0) {
+            hipLaunchKernelGGL((k_relayout<P, N, VB, R>), dim3(grid_for(blocks_len)), dim3(256), 0, s, qa,
+                               blocks_len, occ);
+            return hipGetLastError();
+        } else {
+            return hipErrorInvalidValue;
+        }
+    });
+}
+
+}  // namespace
+
+#if !defined(__HIP_DEVICE_COMPILE__)  // a host table (the device pass only instantiates the kernels)
+#define FMX_OPS_NAME2(p, n) layout_ops_##p##_##n
+#define FMX_OPS_NAME(p, n) FMX_OPS_NAME2(p, n)
+extern const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N);
+const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N) = {op_count, op_search, op_emit, op_dlut_level, op_full_sa,
+                                                           op_relayout};
+#endif
+
+}  // namespace fmx

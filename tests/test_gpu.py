@@ -291,8 +291,11 @@ def test_deep_lut_info(pkg, O):
     text = rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=50_000, p=[.3, .2, .2, .29, .01]).tobytes()
     blob = gpu_build(pkg, text, 5, 4, 3, 64, 3, 2, table)
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    assert ix.info()["options"] == pkg._native.FMX_OPT_DEFAULT == pkg._native.FMX_OCC_INTERLEAVED
+    ix.close()
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=pkg._native.FMX_OPT_DERIVED)
     info = ix.info()
-    assert info["options"] == pkg._native.FMX_OPT_DEFAULT and info["deep_lut_k"] > 3
+    assert info["options"] == pkg._native.FMX_OPT_DERIVED and info["deep_lut_k"] > 3
     K = info["deep_lut_k"]
     pats = [text[s:s + int(rng.integers(1, 3 * K))] for s in rng.integers(0, len(text) - 3 * K, size=3000)]
     pats += [b"NNNNNNNNNNNNNNNN", b"A" * K, b"Z" * (K + 2)]
@@ -532,7 +535,9 @@ def test_fixed_len_hint(pkg, O, m):
         q = [p[::-1] for p in pats] if rev else pats
         data, offsets = pkg.pack_patterns(q)
         cap = int(want[1].size) + 8
-        b = dict(n=n, want=want, data=torch.from_numpy(data.copy()).to(dev),
+        # a wrong (too large) hint below reads n * (m + 1) bytes: fmx.h makes
+        # that the caller's buffer size, so the buffer is padded to it
+        b = dict(n=n, want=want, data=torch.from_numpy(np.concatenate([data, np.zeros(n + 16, np.uint8)])).to(dev),
                  off=torch.from_numpy(offsets.view(np.int64).copy()).to(dev),
                  loff=torch.full((n + 1,), -1, dtype=torch.int64, device=dev),
                  locs=torch.zeros(cap, dtype=torch.int32, device=dev),
@@ -575,3 +580,61 @@ def test_fixed_len_hint(pkg, O, m):
         ix.sync()
     ix.sync()  # the status was cleared by the failing sync
     ix.close()
+
+
+def test_status_is_per_stream(pkg, O):
+    """Device-latched errors belong to the stream whose launch raised them
+    (ADVICE r1): a bad batch (an empty pattern) on stream B and a good one on
+    stream A — fmx_sync(A) is OK, fmx_sync(B) reports FMX_E_EMPTY_PATTERN
+    once, and a later sync of B is OK again."""
+    import torch
+    rng = np.random.default_rng(17)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=50_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    dev = torch.device("cuda:0")
+    sa, sb = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    good = [text[s:s + 12].tobytes() for s in rng.integers(0, text.size - 12, size=3000)]
+    keep = []
+    bad = good[:100] + [b""] + good[100:200]
+    for pats, st in ((good, sa), (bad, sb)):
+        data, offsets = pkg.pack_patterns(pats)
+        n = len(pats)
+        d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
+        o = torch.from_numpy(offsets.view(np.int64).copy()).to(dev)
+        c = torch.zeros(n, dtype=torch.int32, device=dev)
+        st.synchronize()
+        ix.count_batch_async(d.data_ptr(), o.data_ptr(), n, c.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        keep.append((d, o, c))
+    ix.sync(sa.cuda_stream)  # no error on A
+    with pytest.raises(pkg.FmxError) as e:
+        ix.sync(sb.cuda_stream)
+    assert e.value.code == pkg._native.FMX_E_EMPTY_PATTERN
+    ix.sync(sb.cuda_stream)  # reported once, then cleared
+    ix.sync()
+    ix.close()
+
+
+@pytest.mark.parametrize("sigma,budget,pb", [(4, 2 << 20, 4), (5, 32 << 20, 8)])
+def test_max_memory_large_k(pkg, O, sigma, budget, pb):
+    """LookupTableConfig::MaxMemory (lookup_table_config.rs:23-51) with k >= 8:
+    the k-mer count table (1.5 MB / 13 MB) is far past the kernels' LDS copy
+    and is read from HBM; patterns shorter and longer than k, absent k-mers,
+    wildcard bytes — builder bytes and every result equal the oracle's."""
+    rng = np.random.default_rng(sigma * 1000 + pb)
+    chars = b"ACGT" if sigma == 4 else b"ACGTN"
+    table = table_from_symbols([bytes([c]) for c in chars])
+    position = pos_of(pkg, pb)
+    k = pkg.build_config.LookupTableConfig.MaxMemory(budget).kmer_size(position, sigma)
+    assert k >= 8 and (sigma + 1) ** k * pb <= budget < (sigma + 1) ** (k + 1) * pb
+    text = bytes(rng.choice(np.frombuffer(chars, np.uint8), size=300_000))
+    planes, vb = (2, 64) if pb == 4 else (3, 128)
+    blob = gpu_build(pkg, text, sigma, pb, planes, vb, k, 2, table)
+    assert np.array_equal(blob, O.build(text, sigma, O.layout(pb, planes, vb), k, 2, table))
+    pats = [rand_pattern(rng, text, 1, 30) for _ in range(3000)]
+    pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=int(rng.integers(8, 16)))) for _ in range(300)]
+    pats += [b"Z" * 9, b"A" * 12, chars * 3]
+    for occ in (0, 1, 63):
+        check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, reversed_too=(occ == 1))

@@ -1,0 +1,105 @@
+"""Full-size parity on BASELINE.json's configurations (C2, C4, C5): the blob
+is built on the GPU from a seeded synthetic text, copied to the host, and the
+oracle (oracle/fmx_oracle.c, the C restatement of the reference's query path)
+answers the same patterns on the same blob bytes.  Every count and every
+location (suffix-array-row order) of the GPU must equal the oracle's, under
+the faithful index (FMX_OPT_DEFAULT) and every derived structure
+(FMX_OPT_DERIVED).  Sizes are the configs' own: 1 Gbp / 1 G residues / 3 Gbp
+texts; 100,000 patterns each (C5: a 100,000-pattern subset of its 1 M)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ACGTN = [b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"]
+AMINO = b"ACDEFGHIKLMNPQRSTVWY"
+
+
+def progress(msg):
+    print(f"[full] {msg}", flush=True)
+
+
+def oracle_threads():
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def run_config(pkg, O, n, alphabet, symbols, pos, planes, vec, m, npat, seed, extra=()):
+    import torch
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    alpha = torch.tensor(list(alphabet), dtype=torch.uint8, device=dev)
+    d_text = torch.empty(n, dtype=torch.uint8, device=dev)
+    for c0 in range(0, n, 1 << 28):
+        c1 = min(n, c0 + (1 << 28))
+        d_text[c0:c1] = alpha[torch.randint(0, len(alphabet), (c1 - c0,), device=dev, generator=gen)]
+    table = pkg.text_encoders.EncodingTable.from_symbols(symbols)
+    position = pkg.u32 if pos == 4 else pkg.u64
+    block = getattr(pkg.blocks, f"Block{planes}")(pkg.Vector(vec))
+    b = (pkg.FmIndexBuilder(n, table.symbol_count(), table, position, block)
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    size = b.blob_size()
+    d_blob = torch.empty(size, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # (fmx_build_device also waits for the device)
+    b.build_device(d_text.data_ptr(), d_blob.data_ptr(), size)
+    progress(f"n={n:,}: blob {size:,} B built on the GPU")
+    starts = torch.randint(0, n - m + 1, (npat,), device=dev, generator=gen)
+    pats = d_text[(starts[:, None] + torch.arange(m, device=dev)[None, :]).reshape(-1)].cpu().numpy()
+    blob = O.aligned_zeros(size, 16)
+    blob[:] = d_blob.cpu().numpy()
+    del d_text, d_blob
+    torch.cuda.empty_cache()
+    offsets = np.arange(npat + 1, dtype=np.uint64) * m
+    # a few edge patterns: absent, wildcard-only, short (not so short that
+    # they occur millions of times: the oracle walks every row)
+    extra = [bytes(x) for x in extra]
+    if extra:
+        ex_d, ex_o = pkg.pack_patterns(extra)
+        pats = np.concatenate([pats, ex_d])
+        offsets = np.concatenate([offsets, ex_o[1:] + offsets[-1]])
+    orc = O.OracleIndex(blob, O.layout(pos, planes, vec, 0))
+    ooff, olocs = orc.locate_batch(pats, offsets, threads=oracle_threads())
+    cnts = np.diff(ooff)
+    top = np.argsort(cnts)[-3:]
+    progress(f"oracle: {offsets.size - 1:,} patterns, {olocs.size:,} locations; most: "
+             + ", ".join(f"{bytes(pats[int(offsets[i]):int(offsets[i + 1])])!r} x{int(cnts[i])}" for i in top)
+             + f"; zero counts: {int((cnts[:npat] == 0).sum())}")
+    starts_h = starts.cpu().numpy()
+    for options in (pkg._native.FMX_OPT_DEFAULT, pkg._native.FMX_OPT_DERIVED):
+        ix = pkg.FmIndex.load(blob, position, block, table, options=options)
+        goff, glocs = ix.locate_batch((pats, offsets))
+        assert np.array_equal(goff, ooff), f"offsets differ, options {options}"
+        assert np.array_equal(glocs, olocs), f"locations differ, options {options}"
+        cnt = ix.count_batch((pats, offsets))
+        assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff))
+        progress(f"options {options}: bit-exact")
+        ix.close()
+    # the size-independent property: every cut pattern finds its own start
+    own = np.zeros(npat, dtype=bool)
+    cnt = np.diff(ooff[:npat + 1]).astype(np.int64)
+    owner = np.repeat(np.arange(npat), cnt)
+    own[owner[olocs[:owner.size].astype(np.int64) == starts_h[owner]]] = True
+    assert own.all()
+    return ooff, olocs
+
+
+def test_c2_full(pkg, O):
+    """C2: 1 Gbp ACGT (ACGTN table), u32/Block3<u64>, sr 2, k 3, 100,000 x 20 bp."""
+    run_config(pkg, O, 1_000_000_000, b"ACGT", ACGTN, 4, 3, 64, 20, 100_000, 42,
+               extra=[b"N" * 20, b"ACGTNACGTN", b"GATTACA" * 3, b"ACGTACGTACGT"])
+
+
+def test_c4_full(pkg, O):
+    """C4: 1 G residues over 20 amino acids (+X wildcard: sigma 21),
+    u32/Block5<u64>, sr 2, k 3, 100,000 x 12 aa."""
+    run_config(pkg, O, 1_000_000_000, AMINO, [bytes([c, c + 32]) for c in AMINO] + [b"Xx"], 4, 5, 64, 12,
+               100_000, 43, extra=[b"X" * 12, b"WWWWWWWWWWWW", b"MKV", b"ACDEFGHIKLMNPQRSTVWY"])
+
+
+def test_c5_full(pkg, O):
+    """C5: 3 Gbp ACGT, u64/Block3<u128> (ALIGN 16), sr 2, k 3, 100,000 x 150 bp."""
+    run_config(pkg, O, 3_000_000_000, b"ACGT", ACGTN, 8, 3, 128, 150, 100_000, 44,
+               extra=[b"N" * 150, b"ACGT" * 37, b"GATTACAGATTACA"])
