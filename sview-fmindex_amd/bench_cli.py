@@ -252,6 +252,9 @@ def main(argv=None):
     elif a.command == "locate":
         locate(a.data_dir, a.algorithm, a.treat_t_as_wildcard, a.drop_caches, a.batch, a.device, a.options)
     print(f"Total time: {time.perf_counter_ns() - t0} ns")
+    # the reference's run_benchmark.sh reads max RSS from /usr/bin/time -v
+    import resource
+    print(f"Maximum resident set size (kbytes): {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss}")
 
 
 if __name__ == "__main__":
