@@ -12,13 +12,17 @@
 //   4. occ encoding        BwmHeader::encode_bwm_body (bwm/mod.rs:91-143) with
 //                          Block::vectorize / shift_last_offset (blocks/block3.rs:18-39)
 //
-// Sizes: n + 1 < 2^32 (32-bit suffix indices).  Memory: about 40 B per text byte
-// of transient HBM at the peak (keys, values and their double buffers).
+// Sizes: n + 1 < 2^32 with 32-bit suffix indices (about 40 B per text byte of
+// transient HBM at the peak: keys, values and their double buffers); larger
+// texts take the bucketed 64-bit path (suffix_array64: ~17 B per text byte
+// plus ~40 B per element of the largest first-two-symbol bucket).
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "fmx_internal.hpp"
@@ -173,13 +177,15 @@ __global__ __launch_bounds__(256) void k_round_write(const uint32_t *__restrict_
 
 // ------------------------------------------------------- 3. BWT / SA
 
-__global__ void k_find_pidx(const uint32_t *__restrict__ sa, uint64_t n1, unsigned long long *__restrict__ out) {
+template <typename I>
+__global__ void k_find_pidx(const I *__restrict__ sa, uint64_t n1, unsigned long long *__restrict__ out) {
     for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n1; r += (uint64_t)gridDim.x * 256)
         if (sa[r] == 0) *out = r;
 }
 
 // stored BWT = full BWT without the sentinel row pidx (bwt.remove(pidx))
-__global__ __launch_bounds__(256) void k_bwt(const uint8_t *__restrict__ t, const uint32_t *__restrict__ sa, uint64_t n,
+template <typename I>
+__global__ __launch_bounds__(256) void k_bwt(const uint8_t *__restrict__ t, const I *__restrict__ sa, uint64_t n,
                                              const unsigned long long *__restrict__ pidx, uint8_t *__restrict__ bwt) {
     const uint64_t pi = *pidx;
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256) {
@@ -189,8 +195,8 @@ __global__ __launch_bounds__(256) void k_bwt(const uint8_t *__restrict__ t, cons
 }
 
 // sampled SA: SA.remove(0); step_by(sr)  (crate_bio_manual/mod.rs:18-21)
-template <typename P>
-__global__ __launch_bounds__(256) void k_sample_sa(const uint32_t *__restrict__ sa, uint64_t sa_len, uint64_t sr,
+template <typename P, typename I>
+__global__ __launch_bounds__(256) void k_sample_sa(const I *__restrict__ sa, uint64_t sa_len, uint64_t sr,
                                                    P *__restrict__ out) {
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < sa_len; j += (uint64_t)gridDim.x * 256)
         out[j] = (P)sa[1 + j * sr];
@@ -408,6 +414,298 @@ static fmx_status suffix_array(const uint8_t *t, uint64_t n1, uint32_t alphabet,
     return FMX_OK;
 }
 
+
+// ---------------------------------------------- 2b. suffix array, 64-bit
+//
+// For n + 1 >= 2^32 (or FMX_BUILD_SA64=1): the same prefix doubling with
+// 64-bit suffix indices and ranks, made to fit HBM by bucketing the first
+// sort.  Positions are counting-sorted by their first two symbols into `sa`
+// (one bucket = one contiguous slot range); each bucket is then sorted alone
+// by the packed first K0 symbols (64-bit keys), which assigns every slot its
+// group-head rank.  The doubling rounds sort only the unresolved groups: by
+// rank(i + h), then stably by rank(i) (both 64-bit keys, two stable radix
+// sorts: a 128-bit key in two passes).  Transient HBM: t + sa + isa (17 B per
+// text byte) plus ~40 B per element of the largest bucket / active set.
+
+__global__ __launch_bounds__(256) void k_bucket_of(const uint8_t *__restrict__ t, uint64_t n1, uint32_t W,
+                                                   uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t lh[];
+    for (uint32_t b = threadIdx.x; b < W * W; b += 256) lh[b] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n1; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = t[i] * W + (i + 1 < n1 ? t[i + 1] : 0);
+        atomicAdd(&lh[b], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < W * W; b += 256) hist[(uint64_t)blockIdx.x * W * W + b] = lh[b];
+}
+
+// scatter positions into their bucket's slots; base[g * W*W + b] = first slot
+// of workgroup g's positions in bucket b (exclusive scan over (b, g))
+__global__ __launch_bounds__(256) void k_bucket_scatter(const uint8_t *__restrict__ t, uint64_t n1, uint32_t W,
+                                                        const uint64_t *__restrict__ base, uint64_t *__restrict__ sa) {
+    extern __shared__ unsigned long long cur[];
+    for (uint32_t b = threadIdx.x; b < W * W; b += 256) cur[b] = base[(uint64_t)blockIdx.x * W * W + b];
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n1; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = t[i] * W + (i + 1 < n1 ? t[i + 1] : 0);
+        sa[atomicAdd(&cur[b], 1ull)] = i;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_keys64(const uint8_t *__restrict__ t, uint64_t n1, uint32_t b, uint32_t K0,
+                                                const uint64_t *__restrict__ pos, uint64_t m,
+                                                uint64_t *__restrict__ keys, uint64_t *__restrict__ vals) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = pos[j];
+        uint64_t key = 0;
+        for (uint32_t q = 0; q < K0; ++q) key = (key << b) | (i + q < n1 ? t[i + q] : 0);
+        keys[j] = key;
+        vals[j] = i;
+    }
+}
+
+// head flags of a sorted run: hv[j] = j at a group start (keys differ from
+// j-1), else 0; single[j] = the group has one member
+__global__ __launch_bounds__(256) void k_heads64(const uint64_t *__restrict__ k1, const uint64_t *__restrict__ k2,
+                                                 uint64_t m, uint64_t *__restrict__ hv, uint8_t *__restrict__ active) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const bool eq_prev = j > 0 && k1[j - 1] == k1[j] && (!k2 || k2[j - 1] == k2[j]);
+        const bool eq_next = j + 1 < m && k1[j + 1] == k1[j] && (!k2 || k2[j + 1] == k2[j]);
+        hv[j] = eq_prev ? 0ull : j;
+        active[j] = (eq_prev || eq_next) ? 1 : 0;
+    }
+}
+
+// first pass of one bucket (slots s0..s0+m): sa = sorted positions, isa =
+// global slot of the group head, act = 1 on unresolved slots
+__global__ __launch_bounds__(256) void k_bucket_write(const uint64_t *__restrict__ vals, const uint64_t *__restrict__ hj,
+                                                      const uint8_t *__restrict__ flags, uint64_t m, uint64_t s0,
+                                                      uint64_t *__restrict__ sa, uint64_t *__restrict__ isa,
+                                                      uint8_t *__restrict__ act) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        sa[s0 + j] = vals[j];
+        isa[vals[j]] = s0 + hj[j];
+        act[s0 + j] = flags[j];
+    }
+}
+
+// a doubling round's keys for active slot list A: secondary = rank of i + h
+__global__ __launch_bounds__(256) void k_round_sec(const uint64_t *__restrict__ A, uint64_t m,
+                                                   const uint64_t *__restrict__ sa, const uint64_t *__restrict__ isa,
+                                                   uint64_t h, uint64_t *__restrict__ keys, uint64_t *__restrict__ vals) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = sa[A[j]];
+        keys[j] = isa[i + h];
+        vals[j] = i;
+    }
+}
+
+// primary = current group-head rank of each position (after the secondary sort)
+__global__ __launch_bounds__(256) void k_round_pri(const uint64_t *__restrict__ vals, uint64_t m,
+                                                   const uint64_t *__restrict__ isa, uint64_t *__restrict__ pri,
+                                                   uint64_t *__restrict__ idx) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        pri[j] = isa[vals[j]];
+        idx[j] = j;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather2(const uint64_t *__restrict__ perm, uint64_t m,
+                                                 const uint64_t *__restrict__ a, const uint64_t *__restrict__ b,
+                                                 uint64_t *__restrict__ ao, uint64_t *__restrict__ bo) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        ao[j] = a[perm[j]];
+        bo[j] = b[perm[j]];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_round_write64(const uint64_t *__restrict__ A, uint64_t m,
+                                                       const uint64_t *__restrict__ vals, const uint64_t *__restrict__ hj,
+                                                       uint64_t *__restrict__ sa, uint64_t *__restrict__ isa) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m; j += (uint64_t)gridDim.x * 256) {
+        sa[A[j]] = vals[j];
+        isa[vals[j]] = A[hj[j]];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_iota64(uint64_t *__restrict__ v, uint64_t s0, uint64_t m) {
+    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (uint64_t)gridDim.x * 256) v[r] = s0 + r;
+}
+
+template <class K, class V>
+static hipError_t sort_pairs_db(K *&keys, K *&keys_alt, V *&vals, V *&vals_alt, size_t m, unsigned begin_bit,
+                                unsigned end_bit, hipStream_t s) {
+    rocprim::double_buffer<K> kb(keys, keys_alt);
+    rocprim::double_buffer<V> vb(vals, vals_alt);
+    size_t tb = 0;
+    hipError_t e = rocprim::radix_sort_pairs(nullptr, tb, kb, vb, m, begin_bit, end_bit, s);
+    if (e != hipSuccess) return e;
+    e = with_temp(tb, [&](void *tmp) { return rocprim::radix_sort_pairs(tmp, tb, kb, vb, m, begin_bit, end_bit, s); });
+    if (e != hipSuccess) return e;
+    if (kb.current() != keys) std::swap(keys, keys_alt);
+    if (vb.current() != vals) std::swap(vals, vals_alt);
+    return hipSuccess;
+}
+
+static hipError_t max_scan64(const uint64_t *in, uint64_t *out, size_t m, hipStream_t s) {
+    size_t tb = 0;
+    hipError_t e = rocprim::inclusive_scan(nullptr, tb, in, out, m, rocprim::maximum<uint64_t>(), s);
+    if (e != hipSuccess) return e;
+    return with_temp(tb, [&](void *tmp) {
+        return rocprim::inclusive_scan(tmp, tb, in, out, m, rocprim::maximum<uint64_t>(), s);
+    });
+}
+
+// slots j in [s0, s0 + m) with flags[j] set, appended to out[*count...]
+static hipError_t select_slots(const uint8_t *flags, uint64_t s0, uint64_t m, uint64_t *out, uint64_t *d_count,
+                               uint64_t *h_count, hipStream_t s) {
+    DBuf idx;
+    hipError_t e = idx.alloc(m * 8);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iota64, dim3(grid_of(m)), dim3(256), 0, s, idx.as<uint64_t>(), s0, m);
+    size_t tb = 0;
+    e = rocprim::select(nullptr, tb, idx.as<uint64_t>(), flags + s0, out, d_count, m, s);
+    if (e != hipSuccess) return e;
+    e = with_temp(tb, [&](void *tmp) {
+        return rocprim::select(tmp, tb, idx.as<uint64_t>(), flags + s0, out, d_count, m, s);
+    });
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabet, uint64_t *sa, hipStream_t s) {
+    uint32_t b = 1;
+    while ((1u << b) < alphabet) ++b;
+    const uint32_t K0 = 64 / b, W = alphabet, B2 = W * W;
+    DBuf isa, act;
+    BCK(isa.alloc(n1 * 8));
+    BCK(act.alloc(n1));
+    uint64_t *ISA = isa.as<uint64_t>();
+    uint8_t *ACT = act.as<uint8_t>();
+    // ---- bucket by the first two symbols (counting sort into sa) ----------
+    std::vector<uint64_t> bstart(B2 + 1, 0);
+    {
+        const unsigned G = grid_of(n1, 4096);
+        DBuf hist, base;
+        BCK(hist.alloc((uint64_t)G * B2 * 4));
+        BCK(base.alloc((uint64_t)G * B2 * 8));
+        hipLaunchKernelGGL(k_bucket_of, dim3(G), dim3(256), B2 * 4, s, t, n1, W, hist.as<uint32_t>());
+        BCK(hipGetLastError());
+        std::vector<uint32_t> hh((size_t)G * B2);
+        BCK(hipMemcpyAsync(hh.data(), hist.p, hh.size() * 4, hipMemcpyDeviceToHost, s));
+        BCK(hipStreamSynchronize(s));
+        std::vector<uint64_t> hb((size_t)G * B2);
+        uint64_t run = 0;
+        for (uint32_t bk = 0; bk < B2; ++bk) {
+            bstart[bk] = run;
+            for (unsigned g = 0; g < G; ++g) {
+                hb[(size_t)g * B2 + bk] = run;
+                run += hh[(size_t)g * B2 + bk];
+            }
+        }
+        bstart[B2] = run;
+        BCK(hipMemcpyAsync(base.p, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(G), dim3(256), B2 * 8, s, t, n1, W, base.as<uint64_t>(), sa);
+        BCK(hipGetLastError());
+        BCK(hipStreamSynchronize(s));
+    }
+    // ---- each bucket sorted by its packed first K0 symbols -----------------
+    uint64_t mb = 0;
+    for (uint32_t bk = 0; bk < B2; ++bk) mb = std::max(mb, bstart[bk + 1] - bstart[bk]);
+    {
+        DBuf kA, kB, vA, vB, hv, hj, fl;
+        BCK(kA.alloc(mb * 8)); BCK(kB.alloc(mb * 8)); BCK(vA.alloc(mb * 8)); BCK(vB.alloc(mb * 8));
+        BCK(hv.alloc(mb * 8)); BCK(hj.alloc(mb * 8)); BCK(fl.alloc(mb));
+        for (uint32_t bk = 0; bk < B2; ++bk) {
+            const uint64_t s0 = bstart[bk], m = bstart[bk + 1] - s0;
+            if (!m) continue;
+            uint64_t *k1 = kA.as<uint64_t>(), *k2 = kB.as<uint64_t>(), *v1 = vA.as<uint64_t>(), *v2 = vB.as<uint64_t>();
+            hipLaunchKernelGGL(k_keys64, dim3(grid_of(m)), dim3(256), 0, s, t, n1, b, K0, sa + s0, m, k1, v1);
+            BCK(hipGetLastError());
+            BCK(sort_pairs_db(k1, k2, v1, v2, m, 0, b * K0, s));
+            hipLaunchKernelGGL(k_heads64, dim3(grid_of(m)), dim3(256), 0, s, k1, (const uint64_t *)nullptr, m,
+                               hv.as<uint64_t>(), fl.as<uint8_t>());
+            BCK(max_scan64(hv.as<uint64_t>(), hj.as<uint64_t>(), m, s));
+            hipLaunchKernelGGL(k_bucket_write, dim3(grid_of(m)), dim3(256), 0, s, v1, hj.as<uint64_t>(),
+                               fl.as<uint8_t>(), m, s0, sa, ISA, ACT);
+            BCK(hipGetLastError());
+        }
+        BCK(hipStreamSynchronize(s));
+    }
+    // ---- active slots (unresolved groups), collected bucket by bucket ------
+    uint64_t m = 0;
+    DBuf alist, cntd;
+    BCK(cntd.alloc(8));
+    {
+        // size the list: count the flags first (bounded per-bucket selects)
+        std::vector<uint64_t> part(B2, 0);
+        uint64_t total = 0;
+        DBuf tmpl;
+        BCK(tmpl.alloc(std::max<uint64_t>(mb, 1) * 8));
+        for (uint32_t bk = 0; bk < B2; ++bk) {
+            const uint64_t s0 = bstart[bk], mm = bstart[bk + 1] - s0;
+            if (!mm) continue;
+            BCK(select_slots(ACT, s0, mm, tmpl.as<uint64_t>(), cntd.as<uint64_t>(), &part[bk], s));
+            total += part[bk];
+        }
+        BCK(alist.alloc(std::max<uint64_t>(total, 1) * 8));
+        for (uint32_t bk = 0; bk < B2; ++bk) {
+            const uint64_t s0 = bstart[bk], mm = bstart[bk + 1] - s0;
+            if (!part[bk]) continue;
+            uint64_t got = 0;
+            BCK(select_slots(ACT, s0, mm, alist.as<uint64_t>() + m, cntd.as<uint64_t>(), &got, s));
+            m += got;
+        }
+    }
+    act.alloc(0);
+    // ---- doubling rounds over the unresolved groups -------------------------
+    uint64_t *A = alist.as<uint64_t>();
+    for (uint64_t h = K0; m > 0; h *= 2) {
+        if (h >= n1) return FMX_E_CONFIG;  // impossible with a unique sentinel
+        DBuf kA, kB, vA, vB, pri, idx, idx2, sec2, val2, hv, hj, fl, A2;
+        BCK(kA.alloc(m * 8)); BCK(kB.alloc(m * 8)); BCK(vA.alloc(m * 8)); BCK(vB.alloc(m * 8));
+        uint64_t *k1 = kA.as<uint64_t>(), *k2 = kB.as<uint64_t>(), *v1 = vA.as<uint64_t>(), *v2 = vB.as<uint64_t>();
+        hipLaunchKernelGGL(k_round_sec, dim3(grid_of(m)), dim3(256), 0, s, A, m, sa, ISA, h, k1, v1);
+        BCK(hipGetLastError());
+        BCK(sort_pairs_db(k1, k2, v1, v2, m, 0, 64, s));  // by rank(i + h)
+        BCK(pri.alloc(m * 8)); BCK(idx.alloc(m * 8)); BCK(idx2.alloc(m * 8)); BCK(sec2.alloc(m * 8));
+        BCK(val2.alloc(m * 8));
+        uint64_t *p1 = pri.as<uint64_t>(), *p2 = k2, *i1 = idx.as<uint64_t>(), *i2 = idx2.as<uint64_t>();
+        hipLaunchKernelGGL(k_round_pri, dim3(grid_of(m)), dim3(256), 0, s, v1, m, ISA, p1, i1);
+        BCK(hipGetLastError());
+        BCK(sort_pairs_db(p1, p2, i1, i2, m, 0, 64, s));  // stably by rank(i): groups stay in slot order
+        hipLaunchKernelGGL(k_gather2, dim3(grid_of(m)), dim3(256), 0, s, i1, m, v1, k1, val2.as<uint64_t>(),
+                           sec2.as<uint64_t>());
+        BCK(hipGetLastError());
+        BCK(hv.alloc(m * 8)); BCK(hj.alloc(m * 8)); BCK(fl.alloc(m));
+        hipLaunchKernelGGL(k_heads64, dim3(grid_of(m)), dim3(256), 0, s, p1, sec2.as<uint64_t>(), m,
+                           hv.as<uint64_t>(), fl.as<uint8_t>());
+        BCK(max_scan64(hv.as<uint64_t>(), hj.as<uint64_t>(), m, s));
+        hipLaunchKernelGGL(k_round_write64, dim3(grid_of(m)), dim3(256), 0, s, A, m, val2.as<uint64_t>(),
+                           hj.as<uint64_t>(), sa, ISA);
+        BCK(hipGetLastError());
+        // the next round's active slots: A[j] where fl[j]
+        BCK(A2.alloc(m * 8));
+        uint64_t m2 = 0;
+        {
+            size_t tb = 0;
+            BCK(rocprim::select(nullptr, tb, A, fl.as<uint8_t>(), A2.as<uint64_t>(), cntd.as<uint64_t>(), m, s));
+            BCK(with_temp(tb, [&](void *tmp) {
+                return rocprim::select(tmp, tb, A, fl.as<uint8_t>(), A2.as<uint64_t>(), cntd.as<uint64_t>(), m, s);
+            }));
+            BCK(hipMemcpyAsync(&m2, cntd.p, 8, hipMemcpyDeviceToHost, s));
+            BCK(hipStreamSynchronize(s));
+        }
+        BCK(hipMemcpyAsync(A, A2.p, m2 * 8, hipMemcpyDeviceToDevice, s));
+        m = m2;
+    }
+    BCK(hipStreamSynchronize(s));
+    return FMX_OK;
+}
+
 template <typename P>
 static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *table, uint32_t sigma, fmx_layout L,
                               uint32_t k, uint32_t sr, uint8_t *d_blob, const BlobSizes &S, hipStream_t s) {
@@ -482,20 +780,28 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
     kh.alloc(0); khs.alloc(0);
 
     // ---- 2. suffix array (crate_bio_manual/mod.rs:11-12) -----------------
+    // 32-bit suffix indices while n + 1 < 2^32, else the bucketed 64-bit path
+    const char *force64 = getenv("FMX_BUILD_SA64");
+    const bool sa64 = n1 >= 0xFFFFFFFFull || (force64 && atoi(force64) != 0);
     DBuf sab;
-    BCK(sab.alloc(n1 * 4));
-    fmx_status fs = suffix_array(t, n1, (uint32_t)W, sab.as<uint32_t>(), s);
+    BCK(sab.alloc(n1 * (sa64 ? 8 : 4)));
+    fmx_status fs = sa64 ? suffix_array64(t, n1, (uint32_t)W, sab.as<uint64_t>(), s)
+                         : suffix_array(t, n1, (uint32_t)W, sab.as<uint32_t>(), s);
     if (fs) return fs;
 
     // ---- 3. pidx, stored BWT, sampled SA ----------------------------------
     DBuf pid, bw;
     BCK(pid.alloc(8)); BCK(bw.alloc(n ? n : 1));
-    hipLaunchKernelGGL(k_find_pidx, dim3(grid_of(n1)), dim3(256), 0, s, sab.as<uint32_t>(), n1,
-                       pid.as<unsigned long long>());
-    if (n) hipLaunchKernelGGL(k_bwt, dim3(grid_of(n)), dim3(256), 0, s, t, sab.as<uint32_t>(), n,
-                              pid.as<unsigned long long>(), bw.as<uint8_t>());
-    if (S.sa_len) hipLaunchKernelGGL(k_sample_sa<P>, dim3(grid_of(S.sa_len)), dim3(256), 0, s, sab.as<uint32_t>(),
-                                     S.sa_len, (uint64_t)sr, (P *)sa_out);
+    auto bwt_sa = [&](auto *sa_t) {
+        using I = std::remove_const_t<std::remove_pointer_t<decltype(sa_t)>>;
+        hipLaunchKernelGGL(k_find_pidx<I>, dim3(grid_of(n1)), dim3(256), 0, s, sa_t, n1, pid.as<unsigned long long>());
+        if (n) hipLaunchKernelGGL(k_bwt<I>, dim3(grid_of(n)), dim3(256), 0, s, t, sa_t, n,
+                                  pid.as<unsigned long long>(), bw.as<uint8_t>());
+        if (S.sa_len) hipLaunchKernelGGL((k_sample_sa<P, I>), dim3(grid_of(S.sa_len)), dim3(256), 0, s, sa_t,
+                                         S.sa_len, (uint64_t)sr, (P *)sa_out);
+    };
+    if (sa64) bwt_sa(sab.as<uint64_t>());
+    else bwt_sa(sab.as<uint32_t>());
     hipLaunchKernelGGL(k_put_pidx<P>, dim3(1), dim3(1), 0, s, pid.as<unsigned long long>(), (P *)sent);
     BCK(hipGetLastError());
     BCK(hipStreamSynchronize(s));
@@ -561,7 +867,6 @@ fmx_status build_device(const uint8_t *d_text, uint64_t n, const uint8_t *table,
     if (st) return st;
     if (blob_len != S.total) return FMX_E_CONFIG;                      // BuildError::InvalidBlobSize
     if (((uintptr_t)d_blob) % (L.vec_bits == 128 ? 16 : 8)) return FMX_E_ALIGN;  // NotAlignedBlob
-    if (n + 1 >= 0xFFFFFFFFull) return FMX_E_CONFIG;                   // 32-bit suffix indices
     if (L.pos_bytes == 4) return build_typed<uint32_t>(d_text, n, table, sigma, L, k, sr, d_blob, S, s);
     return build_typed<uint64_t>(d_text, n, table, sigma, L, k, sr, d_blob, S, s);
 }

@@ -638,3 +638,21 @@ def test_max_memory_large_k(pkg, O, sigma, budget, pb):
     pats += [b"Z" * 9, b"A" * 12, chars * 3]
     for occ in (0, 1, 63):
         check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, reversed_too=(occ == 1))
+
+
+def test_builder_sa64_small(pkg, O, monkeypatch):
+    """The 64-bit suffix-array path (bucketed prefix doubling, used for
+    n + 1 >= 2^32; forced here with FMX_BUILD_SA64=1) writes the oracle's
+    blob byte for byte: random texts, long runs (many doubling rounds),
+    n % BL == 0, a one-symbol text, several layouts."""
+    monkeypatch.setenv("FMX_BUILD_SA64", "1")
+    rng = np.random.default_rng(64)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    texts = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20000)),
+             b"A" * 5000 + bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=300)) + b"AC" * 3000,
+             b"ACGT" * 64, b"G" * 777, b"N"]
+    for text in texts:
+        for pb, planes, vb, k, sr in [(4, 3, 64, 3, 2), (8, 3, 128, 4, 3), (8, 3, 32, 1, 1)]:
+            blob = gpu_build(pkg, text, 5, pb, planes, vb, k, sr, table)
+            ref = O.build(text, 5, O.layout(pb, planes, vb), k, sr, table)
+            assert np.array_equal(blob, ref), (len(text), pb, planes, vb)

@@ -103,3 +103,86 @@ def test_c5_full(pkg, O):
     """C5: 3 Gbp ACGT, u64/Block3<u128> (ALIGN 16), sr 2, k 3, 100,000 x 150 bp."""
     run_config(pkg, O, 3_000_000_000, b"ACGT", ACGTN, 8, 3, 128, 150, 100_000, 44,
                extra=[b"N" * 150, b"ACGT" * 37, b"GATTACAGATTACA"])
+
+
+def _device_text(n, seed, alphabet=b"ACGT"):
+    import torch
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    alpha = torch.tensor(list(alphabet), dtype=torch.uint8, device=dev)
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    for c0 in range(0, n, 1 << 28):
+        c1 = min(n, c0 + (1 << 28))
+        d[c0:c1] = alpha[torch.randint(0, len(alphabet), (c1 - c0,), device=dev, generator=gen)]
+    return d, gen
+
+
+def test_builder_sa64_matches_sa32(pkg, O, monkeypatch):
+    """200 Mbp (with a long repeat and an N run): the 64-bit suffix-array
+    path and the 32-bit one give byte-identical blobs at a size where both
+    run with many workgroups and large buckets."""
+    import torch
+    n = 200_000_000
+    d_text, _ = _device_text(n, 7)
+    d_text[50_000_000:50_100_000] = d_text[10_000_000:10_100_000]   # a 100 kbp repeat
+    d_text[120_000_000:120_050_000] = ord("N")                       # an N run (wildcard)
+    table = pkg.text_encoders.EncodingTable.from_symbols(ACGTN)
+    b = (pkg.FmIndexBuilder(n, 5, table, pkg.u64, pkg.blocks.Block3(pkg.Vector.U128))
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    size = b.blob_size()
+    blobs = []
+    for force in ("0", "1"):
+        monkeypatch.setenv("FMX_BUILD_SA64", force)
+        d_blob = torch.zeros(size, dtype=torch.uint8, device="cuda:0")
+        b.build_device(d_text.data_ptr(), d_blob.data_ptr(), size)
+        blobs.append(d_blob)
+        progress(f"SA64={force}: built {size:,} B")
+    assert torch.equal(blobs[0], blobs[1])
+
+
+def test_builder_text_beyond_u32(pkg, O):
+    """n + 1 >= 2^32 (4.4 Gbp, u64 / Block3<u128>): the builder takes its
+    64-bit suffix-array path; the blob validates, and 2,000 patterns cut from
+    the text (+ wildcard ones) are answered bit-exactly like the oracle on the
+    same blob, each finding its own start."""
+    import torch
+    n = 4_400_000_000
+    m = 24
+    d_text, gen = _device_text(n, 11)
+    table = pkg.text_encoders.EncodingTable.from_symbols(ACGTN)
+    block = pkg.blocks.Block3(pkg.Vector.U128)
+    b = (pkg.FmIndexBuilder(n, 5, table, pkg.u64, block)
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    size = b.blob_size()
+    d_blob = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    b.build_device(d_text.data_ptr(), d_blob.data_ptr(), size)
+    progress(f"n={n:,}: blob {size:,} B built on the GPU (64-bit suffix indices)")
+    npat = 2000
+    starts = torch.randint(0, n - m + 1, (npat,), device="cuda:0", generator=gen)
+    starts[-1] = n - m  # the text's last 24 symbols
+    pats = d_text[(starts[:, None] + torch.arange(m, device="cuda:0")[None, :]).reshape(-1)].cpu().numpy()
+    del d_text
+    blob = O.aligned_zeros(size, 16)
+    blob[:] = d_blob.cpu().numpy()
+    del d_blob
+    torch.cuda.empty_cache()
+    offsets = np.arange(npat + 1, dtype=np.uint64) * m
+    extra = [b"N" * m, b"ACGTN" * 4]
+    ex_d, ex_o = pkg.pack_patterns(extra)
+    pats = np.concatenate([pats, ex_d])
+    offsets = np.concatenate([offsets, ex_o[1:] + offsets[-1]])
+    orc = O.OracleIndex(blob, O.layout(8, 3, 128, 0))
+    ooff, olocs = orc.locate_batch(pats, offsets, threads=oracle_threads())
+    ix = pkg.FmIndex.load(blob, pkg.u64, block, table)
+    assert ix.info()["text_len"] == n
+    goff, glocs = ix.locate_batch((pats, offsets))
+    assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    ix.close()
+    st = starts.cpu().numpy()
+    for i in range(npat):
+        assert int(st[i]) in set(int(x) for x in olocs[ooff[i]:ooff[i + 1]])
+    progress(f"{npat} patterns bit-exact, every start found")
