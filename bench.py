@@ -115,6 +115,9 @@ def parse():
     ap.add_argument("--batches", type=int, default=32, help="distinct batches cycled (weak-scaling configs)")
     ap.add_argument("--group", type=int, default=8, help="batches per kernel launch (at most 8)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--presorted", action="store_true",
+                    help="experiment: each launch group's patterns pre-sorted by reversed suffix (upper bound of "
+                         "the cache reuse a suffix sort would buy; not a valid headline workload)")
     return ap.parse_args()
 
 
@@ -145,7 +148,8 @@ class Workload:
     stream q % S.  With `slabs`, batch k writes its counts and locations
     straight into slot k % GR of gather slab k // GR."""
 
-    def __init__(self, torch, ix, d_text, n, m, B, batch_ids, P, S, GR, fixed, dev, seed, rank, slabs=None):
+    def __init__(self, torch, ix, d_text, n, m, B, batch_ids, P, S, GR, fixed, dev, seed, rank, slabs=None,
+                 presorted=False):
         self.ix, self.B = ix, B
         pdt = torch.int32 if P == 4 else torch.int64
         self.cap = B + B // 8 + 4096  # checked against every batch's total at warmup
@@ -171,6 +175,22 @@ class Workload:
                 bt["cnt"] = torch.zeros(B, dtype=pdt, device=dev)
                 bt["locs"] = torch.zeros(self.cap, dtype=pdt, device=dev)
             self.batches.append(bt)
+        if presorted:  # experiment: sort each group's patterns by their reversed last 14 symbols
+            code = torch.zeros(256, dtype=torch.int64, device=dev)
+            for i, c in enumerate(b"ACGT"):
+                code[c] = i
+            for g in range(-(-len(self.batches) // GR)):
+                sel = self.batches[g * GR:(g + 1) * GR]
+                st = torch.cat([b["starts"] for b in sel])
+                pats = torch.stack([b["pat"].view(B, m) for b in sel]).view(-1, m).long()
+                key = torch.zeros(st.numel(), dtype=torch.int64, device=dev)
+                for q in range(min(m, 14)):
+                    key = key * 4 + code[pats[:, m - 1 - q]]
+                order = torch.argsort(key)
+                st, pats = st[order], pats[order].to(torch.uint8)
+                for j, b in enumerate(sel):
+                    b["starts"] = st[j * B:(j + 1) * B].contiguous()
+                    b["pat"].copy_(pats[j * B:(j + 1) * B].reshape(-1))
         self.groups = []
         for g in range(-(-len(self.batches) // GR)):
             sel = self.batches[g * GR:(g + 1) * GR]
@@ -298,12 +318,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FMX_BENCH_BACKEND=gloo: a rehearsal of the multi-rank path with several
+    # ranks on one GPU (RCCL needs one device per rank)
+    backend = os.environ.get("FMX_BENCH_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device(f"cuda:{gpu}")
     torch.cuda.set_device(dev)
+    local = gpu
 
     n = args.text_len or cfg["text_len"]
     m = args.pattern_len or cfg["m"]
@@ -381,7 +409,8 @@ def main():
             raise SystemExit("every rank needs the same number of launch groups (use a job of world * GR batches)")
     else:
         NB = -(-max(S * GR, args.batches) // (S * GR)) * (S * GR)  # whole groups on every stream
-        w = Workload(torch, ix, d_text, n, m, B, list(range(NB)), P, S, GR, fixed, dev, args.seed, rank)
+        w = Workload(torch, ix, d_text, n, m, B, list(range(NB)), P, S, GR, fixed, dev, args.seed, rank,
+                     presorted=args.presorted)
         steps = args.steps or 800
     torch.cuda.synchronize()
 
