@@ -115,6 +115,10 @@ def parse():
     ap.add_argument("--batches", type=int, default=32, help="distinct batches cycled (weak-scaling configs)")
     ap.add_argument("--group", type=int, default=8, help="batches per kernel launch (at most 8)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--xcd-partitioned", action="store_true",
+                    help="experiment: each launch group's patterns arranged so that workgroup tile t (XCD t %% 8) "
+                         "holds only patterns whose last 3 symbols fall in class t %% 8 (upper bound of an "
+                         "XCD-aware partition; not a valid headline workload)")
     ap.add_argument("--presorted", action="store_true",
                     help="experiment: each launch group's patterns pre-sorted by reversed suffix (upper bound of "
                          "the cache reuse a suffix sort would buy; not a valid headline workload)")
@@ -149,7 +153,7 @@ class Workload:
     straight into slot k % GR of gather slab k // GR."""
 
     def __init__(self, torch, ix, d_text, n, m, B, batch_ids, P, S, GR, fixed, dev, seed, rank, slabs=None,
-                 presorted=False):
+                 presorted=False, xcd_partitioned=False):
         self.ix, self.B = ix, B
         pdt = torch.int32 if P == 4 else torch.int64
         self.cap = B + B // 8 + 4096  # checked against every batch's total at warmup
@@ -191,6 +195,33 @@ class Workload:
                 for j, b in enumerate(sel):
                     b["starts"] = st[j * B:(j + 1) * B].contiguous()
                     b["pat"].copy_(pats[j * B:(j + 1) * B].reshape(-1))
+        if xcd_partitioned:  # experiment: tile t of a launch holds class-(t % 8) patterns only
+            import numpy as np
+            code = np.zeros(256, np.int64)
+            code[list(b"ACGT")] = [0, 1, 2, 3]
+            T = -(-B // 256)
+            for g in range(-(-len(self.batches) // GR)):
+                sel = self.batches[g * GR:(g + 1) * GR]
+                st = torch.cat([b["starts"] for b in sel]).cpu().numpy()
+                pats = torch.stack([b["pat"].view(B, m) for b in sel]).view(-1, m).cpu().numpy()
+                cls = (code[pats[:, m - 1]] * 16 + code[pats[:, m - 2]] * 4 + code[pats[:, m - 3]]) % 8
+                want = ((np.arange(len(sel))[:, None] * T + np.arange(B)[None, :] // 256) % 8).reshape(-1)
+                order = np.empty(cls.size, np.int64)
+                pools = [list(np.flatnonzero(cls == c)[::-1]) for c in range(8)]
+                spill = []
+                for u in range(cls.size):
+                    pool = pools[want[u]]
+                    if pool:
+                        order[u] = pool.pop()
+                    else:
+                        order[u] = -1
+                        spill.append(u)
+                rest = [x for pl in pools for x in pl]
+                order[spill] = rest
+                st, pats = st[order], pats[order]
+                for j, b in enumerate(sel):
+                    b["starts"] = torch.from_numpy(st[j * B:(j + 1) * B].copy()).to(dev)
+                    b["pat"].copy_(torch.from_numpy(pats[j * B:(j + 1) * B].reshape(-1).copy()).to(dev))
         self.groups = []
         for g in range(-(-len(self.batches) // GR)):
             sel = self.batches[g * GR:(g + 1) * GR]
@@ -410,7 +441,7 @@ def main():
     else:
         NB = -(-max(S * GR, args.batches) // (S * GR)) * (S * GR)  # whole groups on every stream
         w = Workload(torch, ix, d_text, n, m, B, list(range(NB)), P, S, GR, fixed, dev, args.seed, rank,
-                     presorted=args.presorted)
+                     presorted=args.presorted, xcd_partitioned=args.xcd_partitioned)
         steps = args.steps or 800
     torch.cuda.synchronize()
 

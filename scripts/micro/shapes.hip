@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -66,27 +67,39 @@ static void run(const uint8_t *b, uint64_t bytes, uint64_t n, uint64_t *out, hip
         if (it > 0 && ms < best) best = ms;
     }
     const double recs = (double)n * R / (best * 1e-3);
-    printf("{\"buffer_gb\": %.0f, \"lanes\": %llu, \"slot_bytes\": %d, \"loads_per_record\": %d, \"ms\": %.4f, "
+    printf("{\"buffer_gb\": %.3f, \"lanes\": %llu, \"slot_bytes\": %d, \"loads_per_record\": %d, \"ms\": %.4f, "
            "\"grecords_per_s\": %.2f, \"gaccesses_per_s\": %.2f}\n",
            gb, (unsigned long long)n, G, A, best, recs / 1e9, recs * A / 1e9);
     fflush(stdout);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    // argv: buffer sizes in MB (default 1024 8192); a size list selects the
+    // one-record-per-line shapes only (footprint sweep)
     uint64_t *out;
     CK(hipMalloc(&out, 8));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const uint64_t sizes_gb[] = {1, 8};
+    std::vector<uint64_t> sizes_mb = {1024, 8192};
+    if (argc > 1) {
+        sizes_mb.clear();
+        for (int i = 1; i < argc; ++i) sizes_mb.push_back(strtoull(argv[i], nullptr, 10));
+    }
     const uint64_t lanes[] = {500000, 2000000};
-    for (uint64_t gb : sizes_gb) {
-        const uint64_t bytes = gb << 30;
+    for (uint64_t mb : sizes_mb) {
+        const uint64_t bytes = mb << 20;
+        const double gb = (double)mb / 1024.0;
         uint8_t *b;
         CK(hipMalloc(&b, bytes));
         fill<<<4096, 256>>>((uint64_t *)b, bytes / 8);
         CK(hipDeviceSynchronize());
         for (uint64_t n : lanes) {
+            if (argc > 1) {
+                run<1, 128>(b, bytes, n, out, e0, e1, gb);
+                run<2, 64>(b, bytes, n, out, e0, e1, gb);
+                continue;
+            }
             run<1, 64>(b, bytes, n, out, e0, e1, (double)gb);
             run<2, 64>(b, bytes, n, out, e0, e1, (double)gb);
             run<4, 64>(b, bytes, n, out, e0, e1, (double)gb);
