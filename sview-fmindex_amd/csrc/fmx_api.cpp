@@ -7,10 +7,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "fmx_internal.hpp"
 
@@ -225,6 +229,19 @@ struct DeviceGuard {
     }
 };
 
+// FMX_LOAD_TRACE=1: each load stage's wall time on stderr.
+struct LoadTrace {
+    bool on = getenv("FMX_LOAD_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[fmx load] %-22s %9.3f ms\n", what,
+                std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 // The status word of `s`: every stream an index launches on gets a device
 // word of its own, so fmx_sync(s) reads and clears only what that stream's
 // launches latched (stream-ordered), never another stream's.
@@ -431,24 +448,33 @@ fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, i
         memcpy(dst, blob + off, len);
         return true;
     };
+    LoadTrace tr;
     fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
     if (st) return st;
+    tr.mark("parse headers");
     DeviceGuard dg(device);
     if (!dg.ok) return FMX_E_DEVICE;
+    tr.mark("device (first HIP call)");
     fmx_index *ix = new (std::nothrow) fmx_index();
     if (!ix) return FMX_E_DEVICE;
     ix->bv = bv;
     ix->device = device;
     ix->host_blob = blob;
     ix->blob_len = blob_len;
-    if (hipMalloc(&ix->d_blob_owned, blob_len) != hipSuccess ||
-        hipMemcpy(ix->d_blob_owned, blob, blob_len, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&ix->d_blob_owned, blob_len) != hipSuccess) {
         fmx_free(ix);
         return FMX_E_DEVICE;
     }
+    tr.mark("hipMalloc blob");
+    if (hipMemcpy(ix->d_blob_owned, blob, blob_len, hipMemcpyHostToDevice) != hipSuccess) {
+        fmx_free(ix);
+        return FMX_E_DEVICE;
+    }
+    tr.mark("host -> HBM");
     ix->d_blob = ix->d_blob_owned;
     st = finish_load(ix, options);
     if (st) { fmx_free(ix); return st; }
+    tr.mark("finish_load");
     *out = ix;
     return FMX_OK;
 }
@@ -496,28 +522,43 @@ static bool read_full(int fd, uint64_t off, uint64_t len, void *dst) {
     return true;
 }
 
+// File -> HBM through a ring of pinned chunks: each chunk is read by
+// kReadThreads threads (page-cache copies run ~5-10 GB/s per thread) while
+// earlier chunks are in flight to the device on one stream.
 static fmx_status stream_file(int fd, uint64_t len, uint8_t *d_dst, uint64_t chunk) {
+    constexpr int kBufs = 4, kReadThreads = 8;
     hipStream_t s = nullptr;
-    void *buf[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
+    void *buf[kBufs] = {};
+    hipEvent_t ev[kBufs] = {};
+    bool used[kBufs] = {};
     fmx_status st = FMX_OK;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
-    for (int b = 0; b < 2 && st == FMX_OK; ++b)
+    const int nb = (int)std::min<uint64_t>(kBufs, (len + chunk - 1) / std::max<uint64_t>(chunk, 1));
+    for (int b = 0; b < nb && st == FMX_OK; ++b)
         if (hipHostMalloc(&buf[b], chunk, hipHostMallocDefault) != hipSuccess ||
             hipEventCreateWithFlags(&ev[b], hipEventDisableTiming) != hipSuccess)
             st = FMX_E_DEVICE;
-    bool used[2] = {false, false};
     for (uint64_t off = 0, i = 0; st == FMX_OK && off < len; off += chunk, ++i) {
-        const int b = (int)(i & 1);
+        const int b = (int)(i % (uint64_t)nb);
         const uint64_t n = std::min<uint64_t>(chunk, len - off);
         if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { st = FMX_E_DEVICE; break; }
-        if (!read_full(fd, off, n, buf[b])) { st = FMX_E_ARG; break; }
+        // slices of >= 4 MB, page aligned
+        const uint64_t slice = std::max<uint64_t>(align_up((n + kReadThreads - 1) / kReadThreads, 4096), 4ull << 20);
+        std::vector<std::thread> th;
+        std::atomic<bool> ok{true};
+        for (uint64_t o = slice; o < n; o += slice)
+            th.emplace_back([&, o] {
+                if (!read_full(fd, off + o, std::min(slice, n - o), (uint8_t *)buf[b] + o)) ok = false;
+            });
+        if (!read_full(fd, off, std::min(slice, n), buf[b])) ok = false;
+        for (auto &t : th) t.join();
+        if (!ok) { st = FMX_E_ARG; break; }
         if (hipMemcpyAsync(d_dst + off, buf[b], n, hipMemcpyHostToDevice, s) != hipSuccess ||
             hipEventRecord(ev[b], s) != hipSuccess) { st = FMX_E_DEVICE; break; }
         used[b] = true;
     }
     if (hipStreamSynchronize(s) != hipSuccess && st == FMX_OK) st = FMX_E_DEVICE;
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kBufs; ++b) {
         if (ev[b]) hipEventDestroy(ev[b]);
         if (buf[b]) hipHostFree(buf[b]);
     }
@@ -535,14 +576,17 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
     struct stat sb;
     if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close(fd); return FMX_E_ARG; }
     const uint64_t blob_len = (uint64_t)sb.st_size;
+    LoadTrace tr;
     BlobView bv;
     BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
         return off + len <= blob_len && read_full(fd, off, len, dst);
     };
     fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
     if (st) { close(fd); return st; }
+    tr.mark("parse headers");
     DeviceGuard dg(device);
     if (!dg.ok) { close(fd); return FMX_E_DEVICE; }
+    tr.mark("device (first HIP call)");
     fmx_index *ix = new (std::nothrow) fmx_index();
     if (!ix) { close(fd); return FMX_E_DEVICE; }
     ix->bv = bv;
@@ -553,13 +597,16 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
         fmx_free(ix);
         return FMX_E_DEVICE;
     }
+    tr.mark("hipMalloc blob");
     const uint64_t chunk = chunk_bytes ? align_up(chunk_bytes, 4096) : (64ull << 20);
     st = stream_file(fd, blob_len, ix->d_blob_owned, chunk);
     close(fd);
     if (st) { fmx_free(ix); return st; }
+    tr.mark("file -> HBM");
     ix->d_blob = ix->d_blob_owned;
     st = finish_load(ix, options);
     if (st) { fmx_free(ix); return st; }
+    tr.mark("finish_load");
     *out = ix;
     return FMX_OK;
 }
