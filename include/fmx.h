@@ -167,9 +167,10 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
  * bench/src/locate/sview_mmap.rs:17-45 and sview_memory.rs:17-20, then
  * FmIndex::load).  The header is read and validated first (same checks and
  * codes as fmx_load; the file size is the blob length); the body is then
- * streamed file -> pinned host chunks -> HBM, reads overlapping the DMA of
- * the previous chunk, so no host copy of the whole blob is ever held.
- * chunk_bytes = 0 picks the default (64 MiB).  FMX_E_ARG if the file cannot
+ * streamed file -> a ring of four pinned host chunks -> HBM, each chunk read
+ * by several threads while earlier chunks are in flight, so no host copy of
+ * the whole blob is ever held.  chunk_bytes = 0 picks the default (16 MiB:
+ * pinning larger buffers costs more than it saves).  FMX_E_ARG if the file cannot
  * be opened or read.  fmx_blob() returns NULL for such an index. */
 fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32_t options,
                          uint64_t chunk_bytes, fmx_index **out, uint64_t *expected_total,

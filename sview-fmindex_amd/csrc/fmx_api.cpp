@@ -598,7 +598,7 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
         return FMX_E_DEVICE;
     }
     tr.mark("hipMalloc blob");
-    const uint64_t chunk = chunk_bytes ? align_up(chunk_bytes, 4096) : (64ull << 20);
+    const uint64_t chunk = chunk_bytes ? align_up(chunk_bytes, 4096) : (16ull << 20);
     st = stream_file(fd, blob_len, ix->d_blob_owned, chunk);
     close(fd);
     if (st) { fmx_free(ix); return st; }
