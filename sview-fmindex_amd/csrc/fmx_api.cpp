@@ -546,10 +546,16 @@ static fmx_status stream_file(int fd, uint64_t len, uint8_t *d_dst, uint64_t chu
         const uint64_t slice = std::max<uint64_t>(align_up((n + kReadThreads - 1) / kReadThreads, 4096), 4ull << 20);
         std::vector<std::thread> th;
         std::atomic<bool> ok{true};
-        for (uint64_t o = slice; o < n; o += slice)
-            th.emplace_back([&, o] {
+        uint64_t o = slice;
+        try {  // (no exception may leave the C ABI)
+            for (; o < n; o += slice)
+                th.emplace_back([&, o] {
+                    if (!read_full(fd, off + o, std::min(slice, n - o), (uint8_t *)buf[b] + o)) ok = false;
+                });
+        } catch (...) {  // no more threads: this one reads the rest
+            for (; o < n; o += slice)
                 if (!read_full(fd, off + o, std::min(slice, n - o), (uint8_t *)buf[b] + o)) ok = false;
-            });
+        }
         if (!read_full(fd, off, std::min(slice, n), buf[b])) ok = false;
         for (auto &t : th) t.join();
         if (!ok) { st = FMX_E_ARG; break; }

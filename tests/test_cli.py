@@ -128,3 +128,32 @@ def test_load_file_matches_load(pkg, O, tmp_path):
         assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
         assert f.info()["blob_len"] == blob.size
         f.close()
+
+
+@pytest.mark.gpu
+def test_load_file_threaded_ring(pkg, O, tmp_path):
+    """A blob of ~80 MB: the default 16 MiB chunks are read by 4 threads
+    each and the 4-buffer ring wraps several times; a 40 MiB chunk splits
+    into 8 slices with a short last one.  Results equal fmx_load's."""
+    n = 30_000_000
+    rng = np.random.default_rng(12)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=n).astype(np.uint8)
+    table = pkg.text_encoders.EncodingTable.from_symbols([b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"])
+    block = pkg.blocks.Block3(pkg.Vector.U64)
+    b = (pkg.FmIndexBuilder(n, 5, table, pkg.u32, block)
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    blob = pkg.aligned_buffer(b.blob_size())
+    b.build(text, blob)
+    path = str(tmp_path / "big.blob")
+    blob.tofile(path)
+    starts = rng.integers(0, n - 24, size=20000)
+    pats = [text[s:s + int(rng.integers(8, 25))].tobytes() for s in starts]
+    a = pkg.FmIndex.load(blob, pkg.u32, block, table)
+    want = a.locate_batch(pats)
+    a.close()
+    for chunk in (0, 40 << 20, (5 << 20) + 4096):
+        f = pkg.FmIndex.load_file(path, pkg.u32, block, pkg.text_encoders.EncodingTable, chunk_bytes=chunk)
+        got = f.locate_batch(pats)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), f"chunk {chunk}"
+        f.close()
