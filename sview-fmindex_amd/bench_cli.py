@@ -46,13 +46,9 @@ ALGORITHMS = ("sview-memory", "sview-mmap")
 
 def _pkg():
     """The engine package with its library loaded (before any timer, like the
-    reference bench's statically linked binary).  The CLI uses no torch, so
-    libfmx binds the system HIP runtime directly (FMX_NO_TORCH_RUNTIME:
-    importing torch only to share its runtime would add ~1.3 s per process)."""
+    reference bench's statically linked binary)."""
     if _ROOT not in sys.path:
         sys.path.insert(0, _ROOT)
-    if "torch" not in sys.modules:
-        os.environ.setdefault("FMX_NO_TORCH_RUNTIME", "1")
     import __graft_entry__ as g
     pkg = g.load_package()
     pkg._native.lib()
@@ -248,6 +244,12 @@ def locate(data_dir: str, algorithm: str, treat_t_as_wildcard: bool, drop_caches
 
 
 def main(argv=None):
+    # The CLI process uses no torch: libfmx binds the system HIP runtime
+    # directly (importing torch only to share its runtime costs ~1.3 s).  Not
+    # for a process that imports these functions and uses torch itself: two
+    # HIP runtimes in one process do not share the device.
+    if "torch" not in sys.modules:
+        os.environ.setdefault("FMX_NO_TORCH_RUNTIME", "1")
     ap = argparse.ArgumentParser(prog="sview-fmindex-bench (MI355X)")
     sub = ap.add_subparsers(dest="command", required=True)
     g = sub.add_parser("generate")
