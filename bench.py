@@ -54,7 +54,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-RANDOM_LINE_CEILING = 47.0  # G random 64-B line requests/s, 8-128 GB buffers (profiles/r01_randline.jsonl)
+# G dependent random 128-B line reads/s over a 0.5-1 GB buffer (the C2 occ records: 1 GB), 0.5-2 M
+# chains: 52-54 (profiles/r2_footprint.jsonl, profiles/r2_shapes.jsonl; scripts/micro/shapes.hip).
+# Round 1 quoted 47 from 8-128 GB buffers (profiles/r01_randline.jsonl), where TLB reach costs more.
+RANDOM_LINE_CEILING = 52.0
 METRIC = "patterns/sec (count+locate), 1 Gbp text / 20 bp patterns, 1/2/4/8 MI355X"
 FAITHFUL = 1  # FMX_OCC_INTERLEAVED: the blob's own planes and checkpoints, one record per block
 DERIVED = 63  # + deep K-mer table, full SA, text, row contexts, single-row entries
