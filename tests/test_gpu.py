@@ -617,6 +617,65 @@ def test_status_is_per_stream(pkg, O):
     ix.close()
 
 
+def test_concurrent_host_threads(pkg, O):
+    """One index driven from several host threads at once (fmx.h: an index is
+    thread-safe): 4 threads each run the host-buffer API (count + locate,
+    their own pattern sets) and a private-stream async locate with timing on,
+    20 rounds each; every result equals the single-threaded answer."""
+    import threading
+
+    import torch
+    rng = np.random.default_rng(23)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    ix.timing_enable(True)
+    dev = torch.device("cuda:0")
+    sets = []
+    for t in range(4):
+        pats = [text[s:s + int(rng.integers(4, 21))].tobytes() for s in rng.integers(0, text.size - 20, 3000 + 500 * t)]
+        data, offsets = pkg.pack_patterns(pats)
+        want = ix.locate_batch((data, offsets))
+        sets.append((pats, data, offsets, want, ix.count_batch((data, offsets))))
+    errors = []
+
+    def worker(t):
+        try:
+            pats, data, offsets, (wo, wl), wc = sets[t]
+            st = torch.cuda.Stream(device=dev)
+            n = len(pats)
+            d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
+            o = torch.from_numpy(offsets.view(np.int64).copy()).to(dev)
+            loff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            cap = int(wl.size) + 8
+            locs = torch.zeros(cap, dtype=torch.int32, device=dev)
+            need = torch.zeros(1, dtype=torch.int64, device=dev)
+            ws = ix.locate_workspace_size(n)
+            wsb = torch.zeros(ws, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            for _ in range(20):
+                go, gl = ix.locate_batch((data, offsets))
+                assert np.array_equal(go, wo) and np.array_equal(gl, wl)
+                assert np.array_equal(ix.count_batch((data, offsets)), wc)
+                ix.locate_batch_async(d.data_ptr(), o.data_ptr(), n, loff.data_ptr(), locs.data_ptr(), cap,
+                                      need.data_ptr(), wsb.data_ptr(), ws, stream=st.cuda_stream)
+                ix.sync(st.cuda_stream)
+                assert np.array_equal(loff.cpu().numpy().view(np.uint64), wo)
+                assert np.array_equal(locs.cpu().numpy()[:wl.size].view(np.uint32), wl)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    assert ix.timing_read()  # the timers saw the threads' launches
+    ix.close()
+
+
 @pytest.mark.parametrize("sigma,budget,pb", [(4, 2 << 20, 4), (5, 32 << 20, 8)])
 def test_max_memory_large_k(pkg, O, sigma, budget, pb):
     """LookupTableConfig::MaxMemory (lookup_table_config.rs:23-51) with k >= 8:
