@@ -677,6 +677,18 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
     return 0;
 }
 
+// A value read once by one lane (the sampled-SA entry of a walk): a
+// non-temporal load on the device, so that its line does not displace the
+// occ records that other patterns read again.
+template <typename T>
+FMX_HD T load_once(const T *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // Walk one suffix-array row to a sampled row or to the text start
 // (locate/mod.rs:19-35; suffix_array/mod.rs:100-105).
 template <typename P, int N, int VB, int REC>
@@ -696,7 +708,7 @@ FMX_HD P walk_row(const QueryArgs &a, const P *C, P pos) {
         off += 1;
         slot = sr_div(a, (uint64_t)pos, rem);
     }
-    return reinterpret_cast<const P *>(a.sa)[slot] + off;
+    return load_once(reinterpret_cast<const P *>(a.sa) + slot) + off;
 }
 
 
