@@ -142,28 +142,24 @@ def test_builder_sa64_matches_sa32(pkg, O, monkeypatch):
     assert torch.equal(blobs[0], blobs[1])
 
 
-def test_builder_text_beyond_u32(pkg, O):
-    """n + 1 >= 2^32 (4.4 Gbp, u64 / Block3<u128>): the builder takes its
-    64-bit suffix-array path; the blob validates, and 2,000 patterns cut from
-    the text (+ wildcard ones) are answered bit-exactly like the oracle on the
-    same blob, each finding its own start."""
+def _big_text_case(pkg, O, n, position, block, layout, npat=2000, m=24, seed=11):
+    """Build an n-symbol text on the GPU, then answer npat patterns cut from
+    it (the text's last m symbols among them) + wildcard ones like the oracle
+    on the same blob, each finding its own start."""
     import torch
-    n = 4_400_000_000
-    m = 24
-    d_text, gen = _device_text(n, 11)
+    d_text, gen = _device_text(n, seed)
     table = pkg.text_encoders.EncodingTable.from_symbols(ACGTN)
-    block = pkg.blocks.Block3(pkg.Vector.U128)
-    b = (pkg.FmIndexBuilder(n, 5, table, pkg.u64, block)
+    b = (pkg.FmIndexBuilder(n, 5, table, position, block)
          .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
          .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
     size = b.blob_size()
     d_blob = torch.empty(size, dtype=torch.uint8, device="cuda:0")
     torch.cuda.synchronize()
     b.build_device(d_text.data_ptr(), d_blob.data_ptr(), size)
-    progress(f"n={n:,}: blob {size:,} B built on the GPU (64-bit suffix indices)")
-    npat = 2000
+    progress(f"n={n:,}: blob {size:,} B built on the GPU")
     starts = torch.randint(0, n - m + 1, (npat,), device="cuda:0", generator=gen)
-    starts[-1] = n - m  # the text's last 24 symbols
+    starts[-1] = n - m  # the text's last m symbols
+    starts[-2] = 0      # and its first
     pats = d_text[(starts[:, None] + torch.arange(m, device="cuda:0")[None, :]).reshape(-1)].cpu().numpy()
     del d_text
     blob = O.aligned_zeros(size, 16)
@@ -175,9 +171,9 @@ def test_builder_text_beyond_u32(pkg, O):
     ex_d, ex_o = pkg.pack_patterns(extra)
     pats = np.concatenate([pats, ex_d])
     offsets = np.concatenate([offsets, ex_o[1:] + offsets[-1]])
-    orc = O.OracleIndex(blob, O.layout(8, 3, 128, 0))
+    orc = O.OracleIndex(blob, O.layout(*layout, 0))
     ooff, olocs = orc.locate_batch(pats, offsets, threads=oracle_threads())
-    ix = pkg.FmIndex.load(blob, pkg.u64, block, table)
+    ix = pkg.FmIndex.load(blob, position, block, table)
     assert ix.info()["text_len"] == n
     goff, glocs = ix.locate_batch((pats, offsets))
     assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
@@ -186,3 +182,20 @@ def test_builder_text_beyond_u32(pkg, O):
     for i in range(npat):
         assert int(st[i]) in set(int(x) for x in olocs[ooff[i]:ooff[i + 1]])
     progress(f"{npat} patterns bit-exact, every start found")
+
+
+def test_builder_text_beyond_u32(pkg, O):
+    """n + 1 >= 2^32 (4.4 Gbp, u64 / Block3<u128>): the builder takes its
+    64-bit suffix-array path; the blob validates, and 2,000 patterns cut from
+    the text (+ wildcard ones) are answered bit-exactly like the oracle on the
+    same blob, each finding its own start."""
+    _big_text_case(pkg, O, 4_400_000_000, pkg.u64, pkg.blocks.Block3(pkg.Vector.U128), (8, 3, 128))
+
+
+@pytest.mark.parametrize("n", [(1 << 32) - 3, (1 << 32) - 2])
+def test_builder_u32_limit(pkg, O, n):
+    """Both sides of the builder's switch to 64-bit suffix indices (n + 1 =
+    2^32 - 2: the 32-bit path at its last size; n + 1 = 2^32 - 1: the 64-bit
+    path), with u32 positions as close to 2^32 as they go (C[sigma] = n):
+    2,000 patterns answered like the oracle, each finding its own start."""
+    _big_text_case(pkg, O, n, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), (4, 3, 64), seed=13)
