@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 2u
+#define FMX_ABI_VERSION 3u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -130,6 +130,8 @@ typedef struct fmx_index_info {
     int32_t device;
     uint32_t context_len;    /* symbols per row context (0 = no row records)      */
     uint32_t scan_rows;      /* largest interval finished by a record scan        */
+    uint32_t occ_record;     /* occ record encoding: 0 blob layout, 64/128 interleaved
+                                records, | 1 paired-chunk records    */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {

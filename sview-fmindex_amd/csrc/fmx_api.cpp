@@ -301,7 +301,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         const uint32_t rec = interleaved_record_bytes(v);
         if (rec != 0) {
             ix->rec_bytes = rec;
-            ix->occ_bytes = v.blocks_len * rec;
+            ix->occ_bytes = v.blocks_len * (rec & ~15u);
             if (hipMalloc(&ix->d_occ, ix->occ_bytes) != hipSuccess) return FMX_E_DEVICE;
             q.occ = ix->d_occ;
             q.rec_bytes = rec;
@@ -658,6 +658,7 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->deep_lut_k = ix->qa.dlut_k;
     o->context_len = ix->qa.ctx_len;
     o->scan_rows = ix->qa.scan_rows;
+    o->occ_record = ix->occ_mode == FMX_OCC_INTERLEAVED ? ix->rec_bytes : 0;
     o->device = ix->device;
     return FMX_OK;
 }

@@ -118,23 +118,49 @@ using V4 = uint32_t __attribute__((ext_vector_type(4)));
 
 // REC == 0 — blob layout: rank_checkpoints [P; blocks*sigma] and blocks
 //            [BlockN<V>; blocks] are separate arrays (bwm/mod.rs:145-190).
-// REC > 0  — interleaved layout (FMX_OCC_INTERLEAVED): record q (REC = 64 or
-//            128 bytes, REC-aligned) holds block q's N bit planes verbatim at
+// REC = 64 or 128 — interleaved layout (FMX_OCC_INTERLEAVED): record q (REC
+//            bytes, REC-aligned) holds block q's N bit planes verbatim at
 //            [0, PB), then its sigma rank checkpoints as P at PBA + c*P (PBA =
 //            PB rounded up to P), zero padding to REC.  A rank query of
 //            symbol c reads the planes' 16-B chunks and the one chunk holding
 //            checkpoint c — all inside the record's line; when PB is not a
 //            multiple of 16 the planes' last chunk already holds the first
-//            checkpoints (C2, Block3<u64>, u32: 2 chunks for c < 2, 3 else).
+//            checkpoints.
+// REC = 64|kRecPaired or 128|kRecPaired — paired-chunk records, for planes
+//            whose size PB is not a multiple of 16 (tail PT = PB % 16 bytes):
+//            the PF = PB / 16 whole plane chunks, then checkpoint chunks that
+//            each repeat the planes' PT tail bytes followed by PER = (16 -
+//            PTA) / P checkpoints from byte PTA (PT rounded up to P).  Every rank query then reads exactly PF + 1
+//            chunks (C2, Block3<u64>, u32: [p0 p1][p2 ck0 ck1][p2 ck2 ck3]
+//            [p2 ck4 ck5], 2 chunks for every symbol instead of 2 or 3).
+constexpr int kRecPaired = 1;
+
+// Whether record encoding rec (0, 64, 128, 64|kRecPaired, 128|kRecPaired) can
+// hold a block of N planes of VB bits and at least one checkpoint of pos bytes.
+constexpr bool rec_fits(int pos, int N, int VB, int rec) {
+    const int pb = N * VB / 8, rb = rec & ~15;
+    if (rec == 0) return true;
+    const int pta = (pb % 16 + pos - 1) / pos * pos;
+    if (rec & kRecPaired) return pb % 16 != 0 && 16 - pta >= pos && (pb / 16 + 1) * 16 <= rb;
+    return (pb + pos - 1) / pos * pos + pos <= rb;
+}
+
 template <typename P, int N, int VB, int REC>
 struct Occ {
+    static constexpr bool PAIRED = (REC & kRecPaired) != 0;
+    static constexpr int RB = REC & ~15;                                        // record bytes
     static constexpr int PB = N * VB / 8;                                      // plane bytes
     static constexpr int PBA = (PB + (int)sizeof(P) - 1) / (int)sizeof(P) * (int)sizeof(P);
     static constexpr int PBC = (PB + 15) / 16;                                 // chunks holding planes
-    static constexpr int NCH = REC / 16;                                       // chunks per record
-    static constexpr int NCK = REC == 0 ? (1 << N) : (REC - PBA) / (int)sizeof(P);  // checkpoint slots
+    static constexpr int PF = PB / 16, PT = PB % 16;                           // whole plane chunks, tail bytes
+    static constexpr int PTA = (PT + (int)sizeof(P) - 1) / (int)sizeof(P) * (int)sizeof(P);
+    static constexpr int PER = PAIRED ? (16 - PTA) / (int)sizeof(P) : 1;       // checkpoints per paired chunk
+    static constexpr int NCH = RB / 16;                                        // chunks per record
+    static constexpr int NCK = REC == 0 ? (1 << N)
+                             : PAIRED   ? (NCH - PF) * PER
+                                        : (RB - PBA) / (int)sizeof(P);         // checkpoint slots
     static constexpr int NCK2 = pow2_ceil(NCK);
-    static_assert(REC == 0 || PBA + (int)sizeof(P) <= REC, "record too small");
+    static_assert(rec_fits(sizeof(P), N, VB, REC), "record too small");
 
     // One block's planes and one checkpoint, as read for a rank query.
     struct Rec {
@@ -161,14 +187,28 @@ struct Occ {
         else return (P)(d & 2 ? (d & 1 ? v[3] : v[2]) : (d & 1 ? v[1] : v[0]));
     }
 
+    // Checkpoint slot i's chunk and dword within it (compile-time i after unrolling).
+    FMX_HD static constexpr int ck_dword(int i) {
+        return PAIRED ? (PF + i / PER) * 4 + (PTA + (i % PER) * (int)sizeof(P)) / 4 : (PBA + i * (int)sizeof(P)) / 4;
+    }
+
     // The planes of block q and checkpoint c (rank_checkpoints[q*sigma + c]).
     FMX_HD static Rec fetch(const QueryArgs &a, uint64_t q, uint32_t c) {
         Rec r;
         if constexpr (REC == 0) {
             r.ck = reinterpret_cast<const P *>(a.ckpt)[q * a.sigma + c];
             r.pl.load(a.blocks + q * PB);
+        } else if constexpr (PAIRED) {
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
+            V4 ch[PF + 1];
+#pragma unroll
+            for (int i = 0; i < PF; ++i) ch[i] = rp[i];
+            const uint32_t j = c / (uint32_t)PER;
+            ch[PF] = rp[PF + j];  // the planes' tail + checkpoints j*PER ..
+            planes_from(ch, r.pl);
+            r.ck = pick(ch[PF], (uint32_t)(PTA / 4) + (c - j * (uint32_t)PER) * (uint32_t)(sizeof(P) / 4));
         } else {
-            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * REC);
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
             V4 ch[PBC];
 #pragma unroll
             for (int i = 0; i < PBC; ++i) ch[i] = rp[i];
@@ -229,31 +269,41 @@ struct Occ {
                 return ckq[c] + (P)pl.rank(rem, c);
             }
         } else {
-            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * REC);
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
             V4 ch[NCH];
 #pragma unroll
             for (int i = 0; i < NCH; ++i) ch[i] = rp[i];
-            planes_from(ch, pl);
+            planes_from(ch, pl);  // paired: chunk PF (the first checkpoint chunk) holds the tail
             c = pl.sym(rem);
             P all[NCK2];
 #pragma unroll
             for (int i = 0; i < NCK2; ++i) {
-                const int o = PBA + i * (int)sizeof(P);
+                const int d = ck_dword(i);
                 if (i >= NCK) all[i] = P(0);
-                else if constexpr (sizeof(P) == 8) all[i] = (P)((uint64_t)dw(ch, o / 4) | (uint64_t)dw(ch, o / 4 + 1) << 32);
-                else all[i] = (P)dw(ch, o / 4);
+                else if constexpr (sizeof(P) == 8) all[i] = (P)((uint64_t)dw(ch, d) | (uint64_t)dw(ch, d + 1) << 32);
+                else all[i] = (P)dw(ch, d);
             }
             return tree_pick<NCK2>(all, c) + (P)pl.rank(rem, c);
         }
     }
 };
 
-// Interleaved record bytes for a layout (0: too wide, stay on the blob layout).
-FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits, uint32_t sigma) {
+// Interleaved record encoding for a layout (0: too wide, stay on the blob
+// layout): paired-chunk records when the planes leave a tail and they fit the
+// record size the plain layout would take (never larger), else plain 64/128.
+FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits, uint32_t sigma,
+                                      bool paired = true) {
     const uint32_t pb = planes * vec_bits / 8;
     const uint32_t pba = (pb + pos_bytes - 1) / pos_bytes * pos_bytes;
     const uint32_t need = pba + sigma * pos_bytes;
-    return need <= 64 ? 64u : need <= 128 ? 128u : 0u;
+    const uint32_t plain = need <= 64 ? 64u : need <= 128 ? 128u : 0u;
+    const uint32_t pt = pb % 16, pta = (pt + pos_bytes - 1) / pos_bytes * pos_bytes;
+    if (paired && plain != 0 && pt != 0 && 16 - pta >= pos_bytes) {
+        const uint32_t per = (16 - pta) / pos_bytes;
+        const uint32_t bytes = 16 * (pb / 16 + (sigma + per - 1) / per);
+        if (bytes <= plain) return plain | (uint32_t)kRecPaired;
+    }
+    return plain;
 }
 
 // Record q of the interleaved layout from the blob's block q (PB bytes of
@@ -262,20 +312,37 @@ FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint3
 template <typename P, int N, int VB, int REC>
 FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckrow, uint32_t sigma) {
     using O = Occ<P, N, VB, REC>;
-    uint32_t w[REC / 4];
+    constexpr int RB = O::RB;
+    uint32_t w[RB / 4];
 #pragma unroll
-    for (int i = 0; i < REC / 4; ++i) w[i] = 0;
+    for (int i = 0; i < RB / 4; ++i) w[i] = 0;
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(planes);
-#pragma unroll
-    for (int i = 0; i < O::PB / 4; ++i) w[i] = pw[i];
     const uint32_t *cw = reinterpret_cast<const uint32_t *>(ckrow);
-    const uint32_t ncw = sigma * (uint32_t)(sizeof(P) / 4);
+    constexpr int CW = (int)sizeof(P) / 4;  // dwords per checkpoint
+    if constexpr (O::PAIRED) {
 #pragma unroll
-    for (int i = 0; i < (REC - O::PBA) / 4; ++i)
-        if ((uint32_t)i < ncw) w[O::PBA / 4 + i] = cw[i];
+        for (int i = 0; i < O::PF * 4; ++i) w[i] = pw[i];
+#pragma unroll
+        for (int j = O::PF; j < O::NCH; ++j) {
+#pragma unroll
+            for (int i = 0; i < O::PT / 4; ++i) w[4 * j + i] = pw[4 * O::PF + i];
+        }
+#pragma unroll
+        for (int s = 0; s < O::NCK; ++s)
+#pragma unroll
+            for (int i = 0; i < CW; ++i)
+                if ((uint32_t)s < sigma) w[O::ck_dword(s) + i] = cw[s * CW + i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < O::PB / 4; ++i) w[i] = pw[i];
+        const uint32_t ncw = sigma * (uint32_t)CW;
+#pragma unroll
+        for (int i = 0; i < (RB - O::PBA) / 4; ++i)
+            if ((uint32_t)i < ncw) w[O::PBA / 4 + i] = cw[i];
+    }
     V4 *d = reinterpret_cast<V4 *>(dst);
 #pragma unroll
-    for (int i = 0; i < REC / 16; ++i) d[i] = V4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+    for (int i = 0; i < RB / 16; ++i) d[i] = V4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
 }
 
 // ----------------------------------------------------- shared kernel parts

@@ -62,7 +62,7 @@ struct QueryArgs {
     uint32_t sr_pow2, sr_shift;          // sr is a power of two (1 included), log2(sr)
     uint64_t sr_magic;                   // ceil(2^64 / sr) for sr not a power of two
     uint32_t strict;          // PassThrough: bytes >= sigma are an error
-    uint32_t rec_bytes;       // interleaved record size
+    uint32_t rec_bytes;       // interleaved record encoding (bytes | kRecPaired)
     const uint8_t *dlut;      // deep k-mer table: (lo, hi) as P for every dlut_sigma^dlut_k string, or null
     uint32_t dlut_k;
     uint32_t dlut_sigma;      // digits of the table: the symbols that occur in the text (C[c] < C[c+1])

@@ -452,7 +452,7 @@ template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_relayout(const QueryArgs a, uint64_t blocks_len, uint8_t *__restrict__ occ) {
     const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (q >= blocks_len) return;
-    write_record<P, N, VB, REC>(occ + q * REC, a.blocks + q * (N * VB / 8), a.ckpt + q * a.sigma * sizeof(P),
+    write_record<P, N, VB, REC>(occ + q * (REC & ~15), a.blocks + q * (N * VB / 8), a.ckpt + q * a.sigma * sizeof(P),
                                 a.sigma);
 }
 

@@ -1,8 +1,8 @@
 // fmx_layout.hip — the layout-dependent kernels of one (P, N) pair: compiled
 // once per pair (-DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6, csrc/Makefile), each
 // object exporting its LayoutOps table layout_ops_<P>_<N>.  Within a pair the
-// vector width V (32/64/128) and the occ record size (blob layout, 64-B or
-// 128-B interleaved records) are dispatched at run time.
+// vector width V (32/64/128) and the occ record encoding (blob layout, 64-B or
+// 128-B interleaved records, plain or paired-chunk) are dispatched at run time.
 #include "fmx_kernels.hpp"
 
 #if !defined(FMX_LAYOUT_P) || !defined(FMX_LAYOUT_N)
@@ -15,16 +15,20 @@ namespace {
 using P = std::conditional_t<FMX_LAYOUT_P == 4, uint32_t, uint64_t>;
 constexpr int N = FMX_LAYOUT_N;
 
+template <int VB, int R, class F>
+hipError_t disp_if(F &&f) {
+    if constexpr (rec_fits(sizeof(P), N, VB, R)) return f.template operator()<VB, R>();
+    else return hipErrorInvalidValue;
+}
+
 template <int VB, class F>
 hipError_t disp_rec(uint32_t rec, F &&f) {
     switch (rec) {
         case 0: return f.template operator()<VB, 0>();
-        case 64:
-            if constexpr (Occ<P, N, VB, 0>::PBA + (int)sizeof(P) <= 64) return f.template operator()<VB, 64>();
-            else return hipErrorInvalidValue;
-        case 128:
-            if constexpr (Occ<P, N, VB, 0>::PBA + (int)sizeof(P) <= 128) return f.template operator()<VB, 128>();
-            else return hipErrorInvalidValue;
+        case 64: return disp_if<VB, 64>(f);
+        case 128: return disp_if<VB, 128>(f);
+        case 64 | kRecPaired: return disp_if<VB, 64 | kRecPaired>(f);
+        case 128 | kRecPaired: return disp_if<VB, 128 | kRecPaired>(f);
         default: return hipErrorInvalidValue;
     }
 }

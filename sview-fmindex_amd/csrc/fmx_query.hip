@@ -128,8 +128,11 @@ __global__ __launch_bounds__(256) void k_row_ctx(const QueryArgs a, uint64_t n, 
 
 // ------------------------------------------------------------- dispatch
 
+// FMX_OCC_PAIRED=0 keeps the plain record (A/B runs; results are identical)
 uint32_t interleaved_record_bytes(const BlobView &bv) {
-    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma);
+    const char *env = getenv("FMX_OCC_PAIRED");
+    const bool paired = !(env && env[0] == '0');
+    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma, paired);
 }
 
 extern const LayoutOps layout_ops_4_2, layout_ops_4_3, layout_ops_4_4, layout_ops_4_5, layout_ops_4_6,

@@ -53,10 +53,10 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
     // interleaved records (k_relayout)
     std::vector<uint8_t> occ;
     if constexpr (REC != 0) {
-        constexpr int PB = N * VB / 8;
-        occ.assign(ox.blocks_len * REC + 16, 0);
+        constexpr int PB = N * VB / 8, RB = REC & ~15;
+        occ.assign(ox.blocks_len * RB + 16, 0);
         for (uint64_t q = 0; q < ox.blocks_len; ++q)
-            write_record<P, N, VB, REC>(&occ[q * REC], a.blocks + q * PB, a.ckpt + q * ox.sigma * sizeof(P),
+            write_record<P, N, VB, REC>(&occ[q * RB], a.blocks + q * PB, a.ckpt + q * ox.sigma * sizeof(P),
                                         ox.sigma);
         a.occ = occ.data();
     }
@@ -211,18 +211,23 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
     return out > cap ? ORC_E_CAPACITY : ORC_OK;
 }
 
+template <typename P, int N, int VB, int R>
+int run_if(const orc_index &ox, uint32_t options, const uint8_t *b, const uint64_t *o, uint64_t n, uint32_t f,
+           uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need) {
+    if constexpr (rec_fits(sizeof(P), N, VB, R)) return run<P, N, VB, R>(ox, options, b, o, n, f, c, l, cap, need);
+    return -1;
+}
+
 template <typename P, int N, int VB>
 int by_rec(uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b, const uint64_t *o, uint64_t n,
            uint32_t f, uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need) {
-    if (rec == 64) {
-        if constexpr (N * VB / 8 + (int)sizeof(P) <= 64) return run<P, N, VB, 64>(ox, options, b, o, n, f, c, l, cap, need);
-        return -1;
+    switch (rec) {
+        case 64: return run_if<P, N, VB, 64>(ox, options, b, o, n, f, c, l, cap, need);
+        case 128: return run_if<P, N, VB, 128>(ox, options, b, o, n, f, c, l, cap, need);
+        case 64 | kRecPaired: return run_if<P, N, VB, 64 | kRecPaired>(ox, options, b, o, n, f, c, l, cap, need);
+        case 128 | kRecPaired: return run_if<P, N, VB, 128 | kRecPaired>(ox, options, b, o, n, f, c, l, cap, need);
+        default: return run<P, N, VB, 0>(ox, options, b, o, n, f, c, l, cap, need);
     }
-    if (rec == 128) {
-        if constexpr (N * VB / 8 + (int)sizeof(P) <= 128) return run<P, N, VB, 128>(ox, options, b, o, n, f, c, l, cap, need);
-        return -1;
-    }
-    return run<P, N, VB, 0>(ox, options, b, o, n, f, c, l, cap, need);
 }
 
 template <typename P, int N>
@@ -250,7 +255,7 @@ int by_n(const orc_index &ox, uint32_t rec, uint32_t options, const uint8_t *b, 
 extern "C" {
 
 // options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text,
-// 16 row contexts, 32 single-row deep-table entries); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
+// 16 row contexts, 32 single-row deep-table entries; 64 here: plain, not paired-chunk, records); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
 // Outputs are u64: counts[npat] and the concatenated locations.
 int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
                uint32_t encoder, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
@@ -259,11 +264,10 @@ int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t p
     orc_index ox;
     int st = orc_load(blob, len, L, &ox, nullptr, nullptr);
     if (st) return st;
-    uint32_t rec = 0;
-    if (options & 1u) {
-        const uint32_t need = planes * vec_bits / 8 + ox.sigma * pos_bytes;
-        rec = need <= 64 ? 64 : (need <= 128 ? 128 : 0);
-    }
+    // the loader's record choice (k_relayout); options bit 64: plain records only
+    const uint32_t rec = (options & 1u) ? interleaved_rec_bytes(pos_bytes, planes, vec_bits, ox.sigma,
+                                                                (options & 64u) == 0)
+                                        : 0u;
     if (pos_bytes == 4) return by_n<uint32_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
     return by_n<uint64_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
 }
