@@ -131,7 +131,8 @@ typedef struct fmx_index_info {
     uint32_t context_len;    /* symbols per row context (0 = no row records)      */
     uint32_t scan_rows;      /* largest interval finished by a record scan        */
     uint32_t occ_record;     /* occ record encoding: 0 blob layout, 64/128 interleaved
-                                records, | 1 paired-chunk records    */
+                                records, | 1 paired-chunk, | 2 symbol-mask records
+                                                                     */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {

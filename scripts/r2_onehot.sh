@@ -1,0 +1,20 @@
+# Symbol-mask occ records: the record-encoding tests, then faithful A/Bs
+# (one-hot default vs FMX_OCC_ONEHOT=0, i.e. paired/plain) on C2, then C5 and C4 once each.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+T=${TAG:-r2oh}
+timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -x -q -k "record_encodings or readme or golden or every_layout" --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 && echo pytest-ok &&
+ab() {  # tag-suffix, bench args
+  local s=$1; shift
+  for i in 1 2; do
+    for v in onehot paired; do
+      if [ $v = paired ]; then export FMX_OCC_ONEHOT=0; else unset FMX_OCC_ONEHOT; fi
+      timeout -k 10 300 python bench.py --no-derived --no-cpu "$@" > gpurun_out/${T}_${s}_${v}_$i.log 2>&1 || return 1
+      echo "$s $v run $i $(grep -o '"value": [0-9.e+]*' gpurun_out/${T}_${s}_${v}_$i.log | head -1)"
+    done
+  done
+} &&
+ab c2 --min-seconds 0.5 &&
+ab c5 --config c5 &&
+ab c4 --config c4

@@ -130,16 +130,26 @@ using V4 = uint32_t __attribute__((ext_vector_type(4)));
 //            whose size PB is not a multiple of 16 (tail PT = PB % 16 bytes):
 //            the PF = PB / 16 whole plane chunks, then checkpoint chunks that
 //            each repeat the planes' PT tail bytes followed by PER = (16 -
-//            PTA) / P checkpoints from byte PTA (PT rounded up to P).  Every rank query then reads exactly PF + 1
-//            chunks (C2, Block3<u64>, u32: [p0 p1][p2 ck0 ck1][p2 ck2 ck3]
-//            [p2 ck4 ck5], 2 chunks for every symbol instead of 2 or 3).
+//            PTA) / P checkpoints from byte PTA (PT rounded up to P).  Every
+//            rank query then reads exactly PF + 1 chunks (C2, Block3<u64>,
+//            u32: [p0 p1][p2 ck0 ck1][p2 ck2 ck3][p2 ck4 ck5], 2 chunks for
+//            every symbol instead of 2 or 3).
+// REC = 64|kRecOneHot or 128|kRecOneHot — symbol-mask records, when sigma
+//            units fit: unit c (U = VB/8 + P bytes, at c * U) is symbol c's
+//            occurrence mask over the block — the AND of the N planes (or
+//            their complements) that Block::get_remain_count_of forms for c
+//            (block3.rs:42-55), precomputed once per block — followed by the
+//            block's checkpoint c.  A rank query of symbol c is one U-byte
+//            load (C2: 12 B, one dwordx3) and a shift + popcount.
 constexpr int kRecPaired = 1;
+constexpr int kRecOneHot = 2;
 
-// Whether record encoding rec (0, 64, 128, 64|kRecPaired, 128|kRecPaired) can
+// Whether record encoding rec (0, 64, 128, | kRecPaired, | kRecOneHot) can
 // hold a block of N planes of VB bits and at least one checkpoint of pos bytes.
 constexpr bool rec_fits(int pos, int N, int VB, int rec) {
     const int pb = N * VB / 8, rb = rec & ~15;
     if (rec == 0) return true;
+    if (rec & kRecOneHot) return (VB / 8 + pos) % 4 == 0 && 2 * (VB / 8 + pos) <= rb;
     const int pta = (pb % 16 + pos - 1) / pos * pos;
     if (rec & kRecPaired) return pb % 16 != 0 && 16 - pta >= pos && (pb / 16 + 1) * 16 <= rb;
     return (pb + pos - 1) / pos * pos + pos <= rb;
@@ -148,6 +158,8 @@ constexpr bool rec_fits(int pos, int N, int VB, int rec) {
 template <typename P, int N, int VB, int REC>
 struct Occ {
     static constexpr bool PAIRED = (REC & kRecPaired) != 0;
+    static constexpr bool ONEHOT = (REC & kRecOneHot) != 0;
+    static constexpr int U = VB / 8 + (int)sizeof(P);                          // one-hot unit bytes
     static constexpr int RB = REC & ~15;                                        // record bytes
     static constexpr int PB = N * VB / 8;                                      // plane bytes
     static constexpr int PBA = (PB + (int)sizeof(P) - 1) / (int)sizeof(P) * (int)sizeof(P);
@@ -157,6 +169,7 @@ struct Occ {
     static constexpr int PER = PAIRED ? (16 - PTA) / (int)sizeof(P) : 1;       // checkpoints per paired chunk
     static constexpr int NCH = RB / 16;                                        // chunks per record
     static constexpr int NCK = REC == 0 ? (1 << N)
+                             : ONEHOT   ? RB / U
                              : PAIRED   ? (NCH - PF) * PER
                                         : (RB - PBA) / (int)sizeof(P);         // checkpoint slots
     static constexpr int NCK2 = pow2_ceil(NCK);
@@ -190,6 +203,46 @@ struct Occ {
     // Checkpoint slot i's chunk and dword within it (compile-time i after unrolling).
     FMX_HD static constexpr int ck_dword(int i) {
         return PAIRED ? (PF + i / PER) * 4 + (PTA + (i % PER) * (int)sizeof(P)) / 4 : (PBA + i * (int)sizeof(P)) / 4;
+    }
+
+    // One-hot records: symbol c's mask over block q and its checkpoint.
+    struct Hot {
+        uint64_t m0, m1;  // mask words: VB <= 64 in m0; VB = 128 as lo (m0), hi (m1)
+        P ck;
+    };
+    struct Unit {
+        uint32_t d[U / 4];
+    };
+    FMX_HD static Hot hot_from(const uint32_t *d) {
+        Hot h;
+        if constexpr (VB == 32) h.m0 = d[0], h.m1 = 0;
+        else h.m0 = (uint64_t)d[0] | (uint64_t)d[1] << 32, h.m1 = VB == 128 ? ((uint64_t)d[2] | (uint64_t)d[3] << 32) : 0;
+        constexpr int o = VB / 32;
+        if constexpr (sizeof(P) == 8) h.ck = (P)((uint64_t)d[o] | (uint64_t)d[o + 1] << 32);
+        else h.ck = (P)d[o];
+        return h;
+    }
+    FMX_HD static Hot hot_fetch(const QueryArgs &a, uint64_t q, uint32_t c) {
+        const Unit u = *reinterpret_cast<const Unit *>(a.occ + q * RB + c * U);  // one U-byte load
+        return hot_from(u.d);
+    }
+    // occurrences among the block's first rem positions (MSB-first, as Planes::rank)
+    FMX_HD static uint32_t hot_rank(const Hot &h, uint32_t rem) {
+        if (rem == 0) return 0;
+        if constexpr (VB == 128) {
+            if (rem <= 64) return (uint32_t)__builtin_popcountll(h.m1 >> (64 - rem));
+            return (uint32_t)__builtin_popcountll(h.m1) + (uint32_t)__builtin_popcountll(h.m0 >> (128 - rem));
+        } else if constexpr (VB == 64) {
+            return (uint32_t)__builtin_popcountll(h.m0 >> (64 - rem));
+        } else {
+            return (uint32_t)__builtin_popcount((uint32_t)h.m0 >> (32 - rem));
+        }
+    }
+    // whether the mask holds position rem (bit VB - 1 - rem)
+    FMX_HD static bool hot_bit(const Hot &h, uint32_t rem) {
+        const uint32_t b = VB - 1 - rem;
+        if constexpr (VB == 128) return ((b >= 64 ? h.m1 >> (b - 64) : h.m0 >> b) & 1u) != 0;
+        else return ((h.m0 >> b) & 1u) != 0;
     }
 
     // The planes of block q and checkpoint c (rank_checkpoints[q*sigma + c]).
@@ -230,6 +283,10 @@ struct Occ {
     // adjustment (bwm/mod.rs:206-214).  c is known before the loads, so only
     // the planes and the one checkpoint are fetched, all independently.
     FMX_HD static P rank_at(const QueryArgs &a, P p, uint32_t c) {
+        if constexpr (ONEHOT) {
+            const Hot h = hot_fetch(a, (uint64_t)p / VB, c);
+            return h.ck + (P)hot_rank(h, (uint32_t)((uint64_t)p % VB));
+        }
         const Rec r = fetch(a, (uint64_t)p / VB, c);
         return r.ck + (P)r.pl.rank((uint32_t)((uint64_t)p % VB), c);
     }
@@ -240,6 +297,14 @@ struct Occ {
     // a block — that block is read once.
     FMX_HD static void rank_pair(const QueryArgs &a, P plo, P phi, uint32_t c, P &rlo, P &rhi) {
         const uint64_t ql = (uint64_t)plo / VB, qh = (uint64_t)phi / VB;
+        if constexpr (ONEHOT) {
+            const Hot hl = hot_fetch(a, ql, c);
+            Hot hh = hl;
+            if (qh != ql) hh = hot_fetch(a, qh, c);
+            rlo = hl.ck + (P)hot_rank(hl, (uint32_t)((uint64_t)plo % VB));
+            rhi = hh.ck + (P)hot_rank(hh, (uint32_t)((uint64_t)phi % VB));
+            return;
+        }
         const Rec rl = fetch(a, ql, c);
         Rec rh = rl;
         if (qh != ql) rh = fetch(a, qh, c);
@@ -268,6 +333,25 @@ struct Occ {
                 c = pl.sym(rem);
                 return ckq[c] + (P)pl.rank(rem, c);
             }
+        } else if constexpr (ONEHOT) {
+            // the whole record in one round trip; the symbol is the unit whose
+            // mask holds the position
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
+            V4 ch[NCH];
+#pragma unroll
+            for (int i = 0; i < NCH; ++i) ch[i] = rp[i];
+            Hot hs[NCK2];
+            c = 0;
+#pragma unroll
+            for (int i = 0; i < NCK2; ++i) {
+                uint32_t d[U / 4];
+#pragma unroll
+                for (int j = 0; j < U / 4; ++j) d[j] = i < NCK ? dw(ch, i * (U / 4) + j) : 0u;
+                hs[i] = hot_from(d);
+                if (i < NCK && (uint32_t)i < a.sigma && hot_bit(hs[i], rem)) c = (uint32_t)i;
+            }
+            const Hot h = tree_pick<NCK2>(hs, c);
+            return h.ck + (P)hot_rank(h, rem);
         } else {
             const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
             V4 ch[NCH];
@@ -292,11 +376,14 @@ struct Occ {
 // layout): paired-chunk records when the planes leave a tail and they fit the
 // record size the plain layout would take (never larger), else plain 64/128.
 FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits, uint32_t sigma,
-                                      bool paired = true) {
+                                      bool paired = true, bool onehot = true) {
     const uint32_t pb = planes * vec_bits / 8;
     const uint32_t pba = (pb + pos_bytes - 1) / pos_bytes * pos_bytes;
     const uint32_t need = pba + sigma * pos_bytes;
     const uint32_t plain = need <= 64 ? 64u : need <= 128 ? 128u : 0u;
+    const uint32_t u = vec_bits / 8 + pos_bytes, hb = sigma * u;
+    const uint32_t hot = hb <= 64 ? 64u : hb <= 128 ? 128u : 0u;
+    if (onehot && hot != 0 && u % 4 == 0 && (plain == 0 || hot <= plain)) return hot | (uint32_t)kRecOneHot;
     const uint32_t pt = pb % 16, pta = (pt + pos_bytes - 1) / pos_bytes * pos_bytes;
     if (paired && plain != 0 && pt != 0 && 16 - pta >= pos_bytes) {
         const uint32_t per = (16 - pta) / pos_bytes;
@@ -319,7 +406,24 @@ FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckr
     const uint32_t *pw = reinterpret_cast<const uint32_t *>(planes);
     const uint32_t *cw = reinterpret_cast<const uint32_t *>(ckrow);
     constexpr int CW = (int)sizeof(P) / 4;  // dwords per checkpoint
-    if constexpr (O::PAIRED) {
+    if constexpr (O::ONEHOT) {
+        // unit c: the AND over planes j of plane j (bit j of c set) or its
+        // complement — Block::get_remain_count_of's mask — then checkpoint c
+        constexpr int MW = VB / 32;  // mask dwords
+#pragma unroll
+        for (int c = 0; c < O::NCK; ++c) {
+            if ((uint32_t)c >= sigma) break;
+#pragma unroll
+            for (int i = 0; i < MW; ++i) {
+                uint32_t m = ~0u;
+#pragma unroll
+                for (int j = 0; j < N; ++j) m &= ((c >> j) & 1) ? pw[j * MW + i] : ~pw[j * MW + i];
+                w[c * (O::U / 4) + i] = m;
+            }
+#pragma unroll
+            for (int i = 0; i < CW; ++i) w[c * (O::U / 4) + MW + i] = cw[c * CW + i];
+        }
+    } else if constexpr (O::PAIRED) {
 #pragma unroll
         for (int i = 0; i < O::PF * 4; ++i) w[i] = pw[i];
 #pragma unroll

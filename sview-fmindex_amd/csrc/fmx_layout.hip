@@ -2,7 +2,8 @@
 // once per pair (-DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6, csrc/Makefile), each
 // object exporting its LayoutOps table layout_ops_<P>_<N>.  Within a pair the
 // vector width V (32/64/128) and the occ record encoding (blob layout, 64-B or
-// 128-B interleaved records, plain or paired-chunk) are dispatched at run time.
+// 128-B interleaved records: plain, paired-chunk or symbol-mask) are dispatched
+// at run time.
 #include "fmx_kernels.hpp"
 
 #if !defined(FMX_LAYOUT_P) || !defined(FMX_LAYOUT_N)
@@ -29,6 +30,8 @@ hipError_t disp_rec(uint32_t rec, F &&f) {
         case 128: return disp_if<VB, 128>(f);
         case 64 | kRecPaired: return disp_if<VB, 64 | kRecPaired>(f);
         case 128 | kRecPaired: return disp_if<VB, 128 | kRecPaired>(f);
+        case 64 | kRecOneHot: return disp_if<VB, 64 | kRecOneHot>(f);
+        case 128 | kRecOneHot: return disp_if<VB, 128 | kRecOneHot>(f);
         default: return hipErrorInvalidValue;
     }
 }

@@ -128,11 +128,12 @@ __global__ __launch_bounds__(256) void k_row_ctx(const QueryArgs a, uint64_t n, 
 
 // ------------------------------------------------------------- dispatch
 
-// FMX_OCC_PAIRED=0 keeps the plain record (A/B runs; results are identical)
+// FMX_OCC_ONEHOT=0 / FMX_OCC_PAIRED=0 keep the next simpler record encoding
+// (A/B runs; results are identical)
 uint32_t interleaved_record_bytes(const BlobView &bv) {
-    const char *env = getenv("FMX_OCC_PAIRED");
-    const bool paired = !(env && env[0] == '0');
-    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma, paired);
+    const char *ep = getenv("FMX_OCC_PAIRED"), *eh = getenv("FMX_OCC_ONEHOT");
+    const bool paired = !(ep && ep[0] == '0'), onehot = !(eh && eh[0] == '0');
+    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma, paired, onehot);
 }
 
 extern const LayoutOps layout_ops_4_2, layout_ops_4_3, layout_ops_4_4, layout_ops_4_5, layout_ops_4_6,

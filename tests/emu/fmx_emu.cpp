@@ -226,6 +226,8 @@ int by_rec(uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b
         case 128: return run_if<P, N, VB, 128>(ox, options, b, o, n, f, c, l, cap, need);
         case 64 | kRecPaired: return run_if<P, N, VB, 64 | kRecPaired>(ox, options, b, o, n, f, c, l, cap, need);
         case 128 | kRecPaired: return run_if<P, N, VB, 128 | kRecPaired>(ox, options, b, o, n, f, c, l, cap, need);
+        case 64 | kRecOneHot: return run_if<P, N, VB, 64 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
+        case 128 | kRecOneHot: return run_if<P, N, VB, 128 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
         default: return run<P, N, VB, 0>(ox, options, b, o, n, f, c, l, cap, need);
     }
 }
@@ -255,7 +257,7 @@ int by_n(const orc_index &ox, uint32_t rec, uint32_t options, const uint8_t *b, 
 extern "C" {
 
 // options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text,
-// 16 row contexts, 32 single-row deep-table entries; 64 here: plain, not paired-chunk, records); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
+// 16 row contexts, 32 single-row deep-table entries; 64 here: plain records, neither paired-chunk nor symbol-mask); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
 // Outputs are u64: counts[npat] and the concatenated locations.
 int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
                uint32_t encoder, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
@@ -266,7 +268,7 @@ int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t p
     if (st) return st;
     // the loader's record choice (k_relayout); options bit 64: plain records only
     const uint32_t rec = (options & 1u) ? interleaved_rec_bytes(pos_bytes, planes, vec_bits, ox.sigma,
-                                                                (options & 64u) == 0)
+                                                                (options & 64u) == 0, (options & 64u) == 0)
                                         : 0u;
     if (pos_bytes == 4) return by_n<uint32_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
     return by_n<uint64_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);

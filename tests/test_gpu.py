@@ -123,11 +123,15 @@ def test_builder_and_queries_every_layout(pkg, O, pb, planes, vb):
             check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
 
 
-def expected_occ_record(pb, planes, vb, sigma, paired=True):
+def expected_occ_record(pb, planes, vb, sigma, paired=True, onehot=True):
     """The loader's record encoding (fmx_device.hpp interleaved_rec_bytes)."""
     b = planes * vb // 8
     need = -(-b // pb) * pb + sigma * pb
     plain = 64 if need <= 64 else 128 if need <= 128 else 0
+    u = vb // 8 + pb
+    hot = 64 if sigma * u <= 64 else 128 if sigma * u <= 128 else 0
+    if onehot and hot and u % 4 == 0 and (plain == 0 or hot <= plain):
+        return hot | 2
     pt = b % 16
     pta = -(-pt // pb) * pb
     if paired and plain and pt and 16 - pta >= pb:
@@ -138,25 +142,30 @@ def expected_occ_record(pb, planes, vb, sigma, paired=True):
 
 
 @pytest.mark.parametrize("pb,planes,vb", ALL_LAYOUTS)
-def test_paired_and_plain_records(pkg, O, pb, planes, vb, monkeypatch):
-    """Interleaved occ records, paired-chunk (every rank reads planes + one
+def test_record_encodings(pkg, O, pb, planes, vb, monkeypatch):
+    """Interleaved occ records — symbol-mask (one unit per symbol: its mask
+    over the block + checkpoint), paired-chunk (every rank reads planes + one
     checkpoint chunk that repeats the planes' tail) and plain
-    (FMX_OCC_PAIRED=0): the loader picks the expected encoding and both answer
-    like the oracle."""
+    (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0): the loader picks the expected
+    encoding and each answers like the oracle, on random texts and on texts
+    with long single-symbol runs."""
     rng = np.random.default_rng(pb * 7 + planes * 5 + vb)
     for sigma in sorted({2, 3, min(5, 1 << planes), 1 << planes}):
         chars = rand_chr_list(rng, sigma)
         table = table_from_symbols([bytes([c]) for c in chars])
-        text = rand_text(rng, chars, 500, 3000)
-        blob = gpu_build(pkg, text, sigma, pb, planes, vb, 3 if sigma < 8 else 2, 2, table)
-        pats = [rand_pattern(rng, text, 1, 24) for _ in range(300)] + [chars[:1] * 3]
-        for paired in (True, False):
-            monkeypatch.setenv("FMX_OCC_PAIRED", "1" if paired else "0")
-            ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=1)
-            assert ix.info()["occ_record"] == expected_occ_record(pb, planes, vb, sigma, paired), (sigma, paired)
-            ix.close()
-            check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1)
-            check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1 | 2 | 4)
+        for text in (rand_text(rng, chars, 500, 3000),
+                     chars + chars[:1] * 700 + chars * 3 + chars[-1:] * 300 + chars[1:2] * 257):
+            blob = gpu_build(pkg, text, sigma, pb, planes, vb, 3 if sigma < 8 else 2, 2, table)
+            pats = [rand_pattern(rng, text, 1, 24) for _ in range(300)] + [chars[:1] * 3, chars[-1:] * 5]
+            for onehot, paired in ((True, True), (False, True), (False, False)):
+                monkeypatch.setenv("FMX_OCC_ONEHOT", "1" if onehot else "0")
+                monkeypatch.setenv("FMX_OCC_PAIRED", "1" if paired else "0")
+                ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=1)
+                want = expected_occ_record(pb, planes, vb, sigma, paired, onehot)
+                assert ix.info()["occ_record"] == want, (sigma, onehot, paired)
+                ix.close()
+                check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1)
+                check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1 | 2 | 4)
 
 
 @pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 64, 127, 128, 129, 4096])
