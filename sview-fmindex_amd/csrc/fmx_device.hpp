@@ -139,8 +139,11 @@ using V4 = uint32_t __attribute__((ext_vector_type(4)));
 //            occurrence mask over the block — the AND of the N planes (or
 //            their complements) that Block::get_remain_count_of forms for c
 //            (block3.rs:42-55), precomputed once per block — followed by the
-//            block's checkpoint c.  A rank query of symbol c is one U-byte
-//            load (C2: 12 B, one dwordx3) and a shift + popcount.
+//            block's checkpoint c — for VB <= 64 the next block's, i.e. this
+//            one's plus the mask's popcount, so that Occ(c, p) = that minus
+//            popcount(mask << rem) (no special case for rem = 0).  A rank
+//            query of symbol c is one U-byte load (C2: 12 B, one dwordx3, at a
+//            32-bit offset from the records' base) and a shift + popcount.
 constexpr int kRecPaired = 1;
 constexpr int kRecOneHot = 2;
 
@@ -222,20 +225,27 @@ struct Occ {
         else h.ck = (P)d[o];
         return h;
     }
+    // Records of u32 positions with one record per VB positions (RB == VB,
+    // C2: 64-B records of 64 rows) lie below 2^32 bytes for every position
+    // (q * RB <= p & ~(VB - 1) < 2^32): a 32-bit offset from the records' base.
+    static constexpr bool OFF32 = sizeof(P) == 4 && RB == VB;
     FMX_HD static Hot hot_fetch(const QueryArgs &a, uint64_t q, uint32_t c) {
-        const Unit u = *reinterpret_cast<const Unit *>(a.occ + q * RB + c * U);  // one U-byte load
-        return hot_from(u.d);
+        const uint8_t *u;
+        if constexpr (OFF32) u = a.occ + ((uint32_t)q * (uint32_t)RB + c * (uint32_t)U);
+        else u = a.occ + q * RB + c * U;
+        return hot_from(reinterpret_cast<const Unit *>(u)->d);  // one U-byte load
     }
-    // occurrences among the block's first rem positions (MSB-first, as Planes::rank)
-    FMX_HD static uint32_t hot_rank(const Hot &h, uint32_t rem) {
-        if (rem == 0) return 0;
+    // Occ(c, block start + rem): the stored checkpoint and the mask's first rem
+    // positions (MSB-first, as Planes::rank)
+    FMX_HD static P hot_occ(const Hot &h, uint32_t rem) {
         if constexpr (VB == 128) {
-            if (rem <= 64) return (uint32_t)__builtin_popcountll(h.m1 >> (64 - rem));
-            return (uint32_t)__builtin_popcountll(h.m1) + (uint32_t)__builtin_popcountll(h.m0 >> (128 - rem));
+            if (rem == 0) return h.ck;
+            if (rem <= 64) return h.ck + (P)__builtin_popcountll(h.m1 >> (64 - rem));
+            return h.ck + (P)((uint32_t)__builtin_popcountll(h.m1) + (uint32_t)__builtin_popcountll(h.m0 >> (128 - rem)));
         } else if constexpr (VB == 64) {
-            return (uint32_t)__builtin_popcountll(h.m0 >> (64 - rem));
+            return h.ck - (P)__builtin_popcountll(h.m0 << rem);  // ck = next block's checkpoint
         } else {
-            return (uint32_t)__builtin_popcount((uint32_t)h.m0 >> (32 - rem));
+            return h.ck - (P)__builtin_popcount((uint32_t)h.m0 << rem);
         }
     }
     // whether the mask holds position rem (bit VB - 1 - rem)
@@ -285,7 +295,7 @@ struct Occ {
     FMX_HD static P rank_at(const QueryArgs &a, P p, uint32_t c) {
         if constexpr (ONEHOT) {
             const Hot h = hot_fetch(a, (uint64_t)p / VB, c);
-            return h.ck + (P)hot_rank(h, (uint32_t)((uint64_t)p % VB));
+            return hot_occ(h, (uint32_t)((uint64_t)p % VB));
         }
         const Rec r = fetch(a, (uint64_t)p / VB, c);
         return r.ck + (P)r.pl.rank((uint32_t)((uint64_t)p % VB), c);
@@ -301,8 +311,8 @@ struct Occ {
             const Hot hl = hot_fetch(a, ql, c);
             Hot hh = hl;
             if (qh != ql) hh = hot_fetch(a, qh, c);
-            rlo = hl.ck + (P)hot_rank(hl, (uint32_t)((uint64_t)plo % VB));
-            rhi = hh.ck + (P)hot_rank(hh, (uint32_t)((uint64_t)phi % VB));
+            rlo = hot_occ(hl, (uint32_t)((uint64_t)plo % VB));
+            rhi = hot_occ(hh, (uint32_t)((uint64_t)phi % VB));
             return;
         }
         const Rec rl = fetch(a, ql, c);
@@ -351,7 +361,7 @@ struct Occ {
                 if (i < NCK && (uint32_t)i < a.sigma && hot_bit(hs[i], rem)) c = (uint32_t)i;
             }
             const Hot h = tree_pick<NCK2>(hs, c);
-            return h.ck + (P)hot_rank(h, rem);
+            return hot_occ(h, rem);
         } else {
             const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
             V4 ch[NCH];
@@ -420,8 +430,16 @@ FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckr
                 for (int j = 0; j < N; ++j) m &= ((c >> j) & 1) ? pw[j * MW + i] : ~pw[j * MW + i];
                 w[c * (O::U / 4) + i] = m;
             }
+            uint64_t ck = cw[c * CW];
+            if constexpr (CW == 2) ck |= (uint64_t)cw[c * CW + 1] << 32;
+            if constexpr (VB <= 64) {  // the next block's checkpoint: + the mask's popcount
+                uint32_t pc = 0;
 #pragma unroll
-            for (int i = 0; i < CW; ++i) w[c * (O::U / 4) + MW + i] = cw[c * CW + i];
+                for (int i = 0; i < MW; ++i) pc += (uint32_t)__builtin_popcount(w[c * (O::U / 4) + i]);
+                ck += pc;
+            }
+            w[c * (O::U / 4) + MW] = (uint32_t)ck;
+            if constexpr (CW == 2) w[c * (O::U / 4) + MW + 1] = (uint32_t)(ck >> 32);
         }
     } else if constexpr (O::PAIRED) {
 #pragma unroll
