@@ -144,6 +144,12 @@ using V4 = uint32_t __attribute__((ext_vector_type(4)));
 //            popcount(mask << rem) (no special case for rem = 0).  A rank
 //            query of symbol c is one U-byte load (C2: 12 B, one dwordx3, at a
 //            32-bit offset from the records' base) and a shift + popcount.
+//            When sigma units do not fit one line, the record spans L = RB /
+//            128 lines (at most 4) of PL = 128 / U units each (unit c in line
+//            c / PL: a unit never straddles two lines), and the block's planes
+//            sit verbatim at the record's end (last line's spare bytes) for
+//            the walk, which needs the symbol before it can pick a unit
+//            (C4: sigma 21, three lines, 384 B per 64 rows).
 constexpr int kRecPaired = 1;
 constexpr int kRecOneHot = 2;
 
@@ -152,7 +158,13 @@ constexpr int kRecOneHot = 2;
 constexpr bool rec_fits(int pos, int N, int VB, int rec) {
     const int pb = N * VB / 8, rb = rec & ~15;
     if (rec == 0) return true;
-    if (rec & kRecOneHot) return (VB / 8 + pos) % 4 == 0 && 2 * (VB / 8 + pos) <= rb;
+    if (rec & kRecOneHot) {
+        const int u = VB / 8 + pos;
+        if (u % 4 != 0) return false;
+        if (rb <= 128) return 2 * u <= rb;
+        // planes + >= 1 unit in the last line; only where sigma <= 2^N units can overflow one line
+        return rb % 128 == 0 && rb <= 512 && u <= 128 - pb && (1 << N) * u > 128;
+    }
     const int pta = (pb % 16 + pos - 1) / pos * pos;
     if (rec & kRecPaired) return pb % 16 != 0 && 16 - pta >= pos && (pb / 16 + 1) * 16 <= rb;
     return (pb + pos - 1) / pos * pos + pos <= rb;
@@ -171,7 +183,10 @@ struct Occ {
     static constexpr int PTA = (PT + (int)sizeof(P) - 1) / (int)sizeof(P) * (int)sizeof(P);
     static constexpr int PER = PAIRED ? (16 - PTA) / (int)sizeof(P) : 1;       // checkpoints per paired chunk
     static constexpr int NCH = RB / 16;                                        // chunks per record
+    static constexpr bool MULTI = ONEHOT && RB > 128;                        // multi-line symbol masks
+    static constexpr int PL = RB > 128 ? 128 / U : RB / (U > 0 ? U : 1);       // units per line
     static constexpr int NCK = REC == 0 ? (1 << N)
+                             : MULTI    ? (RB / 128 - 1) * PL + (128 - PB) / U
                              : ONEHOT   ? RB / U
                              : PAIRED   ? (NCH - PF) * PER
                                         : (RB - PBA) / (int)sizeof(P);         // checkpoint slots
@@ -232,6 +247,7 @@ struct Occ {
     FMX_HD static Hot hot_fetch(const QueryArgs &a, uint64_t q, uint32_t c) {
         const uint8_t *u;
         if constexpr (OFF32) u = a.occ + ((uint32_t)q * (uint32_t)RB + c * (uint32_t)U);
+        else if constexpr (MULTI) u = a.occ + q * RB + (c / (uint32_t)PL) * 128u + (c % (uint32_t)PL) * (uint32_t)U;
         else u = a.occ + q * RB + c * U;
         return hot_from(reinterpret_cast<const Unit *>(u)->d);  // one U-byte load
     }
@@ -343,6 +359,11 @@ struct Occ {
                 c = pl.sym(rem);
                 return ckq[c] + (P)pl.rank(rem, c);
             }
+        } else if constexpr (MULTI) {
+            // the symbol from the planes kept at the record's end, then its unit
+            pl.load(a.occ + q * RB + (RB - PB));
+            c = pl.sym(rem);
+            return hot_occ(hot_fetch(a, q, c), rem);
         } else if constexpr (ONEHOT) {
             // the whole record in one round trip; the symbol is the unit whose
             // mask holds the position
@@ -394,6 +415,12 @@ FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint3
     const uint32_t u = vec_bits / 8 + pos_bytes, hb = sigma * u;
     const uint32_t hot = hb <= 64 ? 64u : hb <= 128 ? 128u : 0u;
     if (onehot && hot != 0 && u % 4 == 0 && (plain == 0 || hot <= plain)) return hot | (uint32_t)kRecOneHot;
+    if (onehot && hot == 0 && u % 4 == 0 && u <= 128 - pb) {
+        // multi-line: PL units per line, the planes in the last line's spare bytes
+        const uint32_t pl = 128 / u, last_cap = (128 - pb) / u;
+        for (uint32_t l = 2; l <= 4; ++l)
+            if (sigma <= (l - 1) * pl + last_cap) return 128 * l | (uint32_t)kRecOneHot;
+    }
     const uint32_t pt = pb % 16, pta = (pt + pos_bytes - 1) / pos_bytes * pos_bytes;
     if (paired && plain != 0 && pt != 0 && 16 - pta >= pos_bytes) {
         const uint32_t per = (16 - pta) / pos_bytes;
@@ -420,26 +447,29 @@ FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckr
         // unit c: the AND over planes j of plane j (bit j of c set) or its
         // complement — Block::get_remain_count_of's mask — then checkpoint c
         constexpr int MW = VB / 32;  // mask dwords
+        if constexpr (O::MULTI)
+            for (int i = 0; i < O::PB / 4; ++i) w[(RB - O::PB) / 4 + i] = pw[i];
 #pragma unroll
         for (int c = 0; c < O::NCK; ++c) {
             if ((uint32_t)c >= sigma) break;
+            const int ub = O::MULTI ? (c / O::PL) * 32 + (c % O::PL) * (O::U / 4) : c * (O::U / 4);  // unit dword
 #pragma unroll
             for (int i = 0; i < MW; ++i) {
                 uint32_t m = ~0u;
 #pragma unroll
                 for (int j = 0; j < N; ++j) m &= ((c >> j) & 1) ? pw[j * MW + i] : ~pw[j * MW + i];
-                w[c * (O::U / 4) + i] = m;
+                w[ub + i] = m;
             }
             uint64_t ck = cw[c * CW];
             if constexpr (CW == 2) ck |= (uint64_t)cw[c * CW + 1] << 32;
             if constexpr (VB <= 64) {  // the next block's checkpoint: + the mask's popcount
                 uint32_t pc = 0;
 #pragma unroll
-                for (int i = 0; i < MW; ++i) pc += (uint32_t)__builtin_popcount(w[c * (O::U / 4) + i]);
+                for (int i = 0; i < MW; ++i) pc += (uint32_t)__builtin_popcount(w[ub + i]);
                 ck += pc;
             }
-            w[c * (O::U / 4) + MW] = (uint32_t)ck;
-            if constexpr (CW == 2) w[c * (O::U / 4) + MW + 1] = (uint32_t)(ck >> 32);
+            w[ub + MW] = (uint32_t)ck;
+            if constexpr (CW == 2) w[ub + MW + 1] = (uint32_t)(ck >> 32);
         }
     } else if constexpr (O::PAIRED) {
 #pragma unroll

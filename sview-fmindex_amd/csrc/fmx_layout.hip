@@ -32,6 +32,9 @@ hipError_t disp_rec(uint32_t rec, F &&f) {
         case 128 | kRecPaired: return disp_if<VB, 128 | kRecPaired>(f);
         case 64 | kRecOneHot: return disp_if<VB, 64 | kRecOneHot>(f);
         case 128 | kRecOneHot: return disp_if<VB, 128 | kRecOneHot>(f);
+        case 256 | kRecOneHot: return disp_if<VB, 256 | kRecOneHot>(f);
+        case 384 | kRecOneHot: return disp_if<VB, 384 | kRecOneHot>(f);
+        case 512 | kRecOneHot: return disp_if<VB, 512 | kRecOneHot>(f);
         default: return hipErrorInvalidValue;
     }
 }

@@ -228,6 +228,9 @@ int by_rec(uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b
         case 128 | kRecPaired: return run_if<P, N, VB, 128 | kRecPaired>(ox, options, b, o, n, f, c, l, cap, need);
         case 64 | kRecOneHot: return run_if<P, N, VB, 64 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
         case 128 | kRecOneHot: return run_if<P, N, VB, 128 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
+        case 256 | kRecOneHot: return run_if<P, N, VB, 256 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
+        case 384 | kRecOneHot: return run_if<P, N, VB, 384 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
+        case 512 | kRecOneHot: return run_if<P, N, VB, 512 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
         default: return run<P, N, VB, 0>(ox, options, b, o, n, f, c, l, cap, need);
     }
 }

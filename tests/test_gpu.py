@@ -132,6 +132,10 @@ def expected_occ_record(pb, planes, vb, sigma, paired=True, onehot=True):
     hot = 64 if sigma * u <= 64 else 128 if sigma * u <= 128 else 0
     if onehot and hot and u % 4 == 0 and (plain == 0 or hot <= plain):
         return hot | 2
+    if onehot and not hot and u % 4 == 0 and u <= 128 - b:   # multi-line symbol masks
+        for lines in (2, 3, 4):
+            if sigma <= (lines - 1) * (128 // u) + (128 - b) // u:
+                return 128 * lines | 2
     pt = b % 16
     pta = -(-pt // pb) * pb
     if paired and plain and pt and 16 - pta >= pb:
