@@ -298,7 +298,8 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     }
     ix->occ_mode = FMX_OCC_BLOB;
     if (options & FMX_OCC_INTERLEAVED) {
-        const uint32_t rec = interleaved_record_bytes(v);
+        // multi-line symbol masks only for the faithful index (no derived structures)
+        const uint32_t rec = interleaved_record_bytes(v, (options & ~FMX_OCC_INTERLEAVED) == 0);
         if (rec != 0) {
             ix->rec_bytes = rec;
             ix->occ_bytes = v.blocks_len * (rec & ~15u);

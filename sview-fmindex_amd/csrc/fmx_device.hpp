@@ -404,10 +404,11 @@ struct Occ {
 };
 
 // Interleaved record encoding for a layout (0: too wide, stay on the blob
-// layout): paired-chunk records when the planes leave a tail and they fit the
+// layout; multi: whether multi-line symbol masks may be picked — only for the
+// faithful index, the derived kernels are not built for them): paired-chunk records when the planes leave a tail and they fit the
 // record size the plain layout would take (never larger), else plain 64/128.
 FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits, uint32_t sigma,
-                                      bool paired = true, bool onehot = true) {
+                                      bool paired = true, bool onehot = true, bool multi = true) {
     const uint32_t pb = planes * vec_bits / 8;
     const uint32_t pba = (pb + pos_bytes - 1) / pos_bytes * pos_bytes;
     const uint32_t need = pba + sigma * pos_bytes;
@@ -415,7 +416,7 @@ FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint3
     const uint32_t u = vec_bits / 8 + pos_bytes, hb = sigma * u;
     const uint32_t hot = hb <= 64 ? 64u : hb <= 128 ? 128u : 0u;
     if (onehot && hot != 0 && u % 4 == 0 && (plain == 0 || hot <= plain)) return hot | (uint32_t)kRecOneHot;
-    if (onehot && hot == 0 && u % 4 == 0 && u <= 128 - pb) {
+    if (onehot && multi && hot == 0 && u % 4 == 0 && u <= 128 - pb) {
         // multi-line: PL units per line, the planes in the last line's spare bytes
         const uint32_t pl = 128 / u, last_cap = (128 - pb) / u;
         for (uint32_t l = 2; l <= 4; ++l)
@@ -449,8 +450,7 @@ FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckr
         constexpr int MW = VB / 32;  // mask dwords
         if constexpr (O::MULTI)
             for (int i = 0; i < O::PB / 4; ++i) w[(RB - O::PB) / 4 + i] = pw[i];
-#pragma unroll
-        for (int c = 0; c < O::NCK; ++c) {
+        for (int c = 0; c < O::NCK; ++c) {  // (load time only; not unrolled)
             if ((uint32_t)c >= sigma) break;
             const int ub = O::MULTI ? (c / O::PL) * 32 + (c % O::PL) * (O::U / 4) : c * (O::U / 4);  // unit dword
 #pragma unroll

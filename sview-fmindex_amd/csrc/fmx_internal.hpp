@@ -213,7 +213,7 @@ hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream);
 hipError_t build_text(fmx_index *ix, hipStream_t stream);
 // Fill the context half of the row records (FMX_OPT_ROW_CONTEXT) from d_text.
 hipError_t build_row_context(fmx_index *ix, hipStream_t stream);
-uint32_t interleaved_record_bytes(const BlobView &bv);
+uint32_t interleaved_record_bytes(const BlobView &bv, bool multi);
 
 // GPU builder (fmx_build.hip).
 fmx_status build_device(const uint8_t *d_text, uint64_t n, const uint8_t *table, uint32_t sigma,

@@ -1,13 +1,14 @@
-// fmx_layout.hip — the layout-dependent kernels of one (P, N) pair: compiled
-// once per pair (-DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6, csrc/Makefile), each
-// object exporting its LayoutOps table layout_ops_<P>_<N>.  Within a pair the
-// vector width V (32/64/128) and the occ record encoding (blob layout, 64-B or
+// fmx_layout.hip — the layout-dependent kernels of one (P, N, V) triple:
+// compiled once per triple (-DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6
+// -DFMX_LAYOUT_VB=32|64|128, csrc/Makefile: 30 objects built in parallel), each
+// exporting its LayoutOps table layout_ops_<P>_<N>_<V>.  Within a triple the
+// occ record encoding (blob layout, 64-B or
 // 128-B interleaved records: plain, paired-chunk or symbol-mask) are dispatched
 // at run time.
 #include "fmx_kernels.hpp"
 
-#if !defined(FMX_LAYOUT_P) || !defined(FMX_LAYOUT_N)
-#error "build with -DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6"
+#if !defined(FMX_LAYOUT_P) || !defined(FMX_LAYOUT_N) || !defined(FMX_LAYOUT_VB)
+#error "build with -DFMX_LAYOUT_P=4|8 -DFMX_LAYOUT_N=2..6 -DFMX_LAYOUT_VB=32|64|128"
 #endif
 
 namespace fmx {
@@ -39,33 +40,33 @@ hipError_t disp_rec(uint32_t rec, F &&f) {
     }
 }
 
-// f.template operator()<VB, REC>() for the layout's vector width and record size
+// Multi-line symbol-mask records are picked for the faithful index only
+// (fmx_load): their kernels exist in the faithful variant alone.
+constexpr bool faithful_only(int rec) { return (rec & kRecOneHot) != 0 && (rec & ~15) > 128; }
+
+// f.template operator()<VB, REC>() for this object's vector width and the record size
 template <class F>
 hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
-    switch (vb) {
-        case 32: return disp_rec<32>(rec, f);
-        case 64: return disp_rec<64>(rec, f);
-        case 128: return disp_rec<128>(rec, f);
-        default: return hipErrorInvalidValue;
-    }
+    if (vb != FMX_LAYOUT_VB) return hipErrorInvalidValue;
+    return disp_rec<FMX_LAYOUT_VB>(rec, f);
 }
 
 [[maybe_unused]] hipError_t op_count(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const uint8_t *bytes,
                     const uint64_t *offs, uint64_t n, uint32_t flags, void *counts, uint32_t sb, hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
         const uint32_t lds = sb + qa.kt_lds_bytes;
-        switch (var) {
-            case kVarFaithful:
-                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarFaithful>), dim3(grid_for(n)), dim3(256), lds, s, qa,
-                                   bytes, offs, n, flags, (P *)counts, sb);
-                break;
-            case kVarDerived:
-                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerived>), dim3(grid_for(n)), dim3(256), lds, s, qa,
-                                   bytes, offs, n, flags, (P *)counts, sb);
-                break;
-            default:
-                hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerivedLong>), dim3(grid_for(n)), dim3(256), lds, s,
-                                   qa, bytes, offs, n, flags, (P *)counts, sb);
+        const dim3 g(grid_for(n)), b(256);
+        if (var == kVarFaithful) {
+            hipLaunchKernelGGL((k_count<P, N, VB, R, kVarFaithful>), g, b, lds, s, qa, bytes, offs, n, flags,
+                               (P *)counts, sb);
+        } else if constexpr (faithful_only(R)) {
+            return hipErrorInvalidValue;
+        } else if (var == kVarDerived) {
+            hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerived>), g, b, lds, s, qa, bytes, offs, n, flags,
+                               (P *)counts, sb);
+        } else {
+            hipLaunchKernelGGL((k_count<P, N, VB, R, kVarDerivedLong>), g, b, lds, s, qa, bytes, offs, n, flags,
+                               (P *)counts, sb);
         }
         return hipGetLastError();
     });
@@ -75,18 +76,15 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
                      uint32_t tiles, uint32_t sb, hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
         const uint32_t lds = sb + qa.kt_lds_bytes;
-        switch (var) {
-            case kVarFaithful:
-                hipLaunchKernelGGL((k_search<P, N, VB, R, kVarFaithful>), dim3(tiles), dim3(256), lds, s, qa, grp,
-                                   sb);
-                break;
-            case kVarDerived:
-                hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerived>), dim3(tiles), dim3(256), lds, s, qa, grp,
-                                   sb);
-                break;
-            default:
-                hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerivedLong>), dim3(tiles), dim3(256), lds, s, qa,
-                                   grp, sb);
+        if (var == kVarFaithful) {
+            hipLaunchKernelGGL((k_search<P, N, VB, R, kVarFaithful>), dim3(tiles), dim3(256), lds, s, qa, grp, sb);
+        } else if constexpr (faithful_only(R)) {
+            return hipErrorInvalidValue;
+        } else if (var == kVarDerived) {
+            hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerived>), dim3(tiles), dim3(256), lds, s, qa, grp, sb);
+        } else {
+            hipLaunchKernelGGL((k_search<P, N, VB, R, kVarDerivedLong>), dim3(tiles), dim3(256), lds, s, qa, grp,
+                               sb);
         }
         return hipGetLastError();
     });
@@ -103,18 +101,26 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 [[maybe_unused]] hipError_t op_dlut_level(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
                          void *child, hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
-        hipLaunchKernelGGL((k_dlut_level<P, N, VB, R>), dim3(grid_dlut(np)), dim3(256), 0, s, qa,
-                           (const P *)parent, np, (P *)child);
-        return hipGetLastError();
+        if constexpr (faithful_only(R)) {
+            return hipErrorInvalidValue;
+        } else {
+            hipLaunchKernelGGL((k_dlut_level<P, N, VB, R>), dim3(grid_dlut(np)), dim3(256), 0, s, qa,
+                               (const P *)parent, np, (P *)child);
+            return hipGetLastError();
+        }
     });
 }
 
 [[maybe_unused]] hipError_t op_full_sa(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t n, void *sa_out, uint32_t stride,
                       hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
-        hipLaunchKernelGGL((k_full_sa<P, N, VB, R>), dim3(grid_stride_for(n)), dim3(256), 0, s, qa, n,
-                           (P *)sa_out, stride);
-        return hipGetLastError();
+        if constexpr (faithful_only(R)) {
+            return hipErrorInvalidValue;
+        } else {
+            hipLaunchKernelGGL((k_full_sa<P, N, VB, R>), dim3(grid_stride_for(n)), dim3(256), 0, s, qa, n,
+                               (P *)sa_out, stride);
+            return hipGetLastError();
+        }
     });
 }
 
@@ -134,10 +140,10 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 }  // namespace
 
 #if !defined(__HIP_DEVICE_COMPILE__)  // a host table (the device pass only instantiates the kernels)
-#define FMX_OPS_NAME2(p, n) layout_ops_##p##_##n
-#define FMX_OPS_NAME(p, n) FMX_OPS_NAME2(p, n)
-extern const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N);
-const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N) = {op_count, op_search, op_emit, op_dlut_level, op_full_sa,
+#define FMX_OPS_NAME2(p, n, v) layout_ops_##p##_##n##_##v
+#define FMX_OPS_NAME(p, n, v) FMX_OPS_NAME2(p, n, v)
+extern const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB);
+const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB) = {op_count, op_search, op_emit, op_dlut_level, op_full_sa,
                                                            op_relayout};
 #endif
 

@@ -130,14 +130,19 @@ __global__ __launch_bounds__(256) void k_row_ctx(const QueryArgs a, uint64_t n, 
 
 // FMX_OCC_ONEHOT=0 / FMX_OCC_PAIRED=0 keep the next simpler record encoding
 // (A/B runs; results are identical)
-uint32_t interleaved_record_bytes(const BlobView &bv) {
+uint32_t interleaved_record_bytes(const BlobView &bv, bool multi) {
     const char *ep = getenv("FMX_OCC_PAIRED"), *eh = getenv("FMX_OCC_ONEHOT");
     const bool paired = !(ep && ep[0] == '0'), onehot = !(eh && eh[0] == '0');
-    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma, paired, onehot);
+    return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma, paired, onehot, multi);
 }
 
-extern const LayoutOps layout_ops_4_2, layout_ops_4_3, layout_ops_4_4, layout_ops_4_5, layout_ops_4_6,
-    layout_ops_8_2, layout_ops_8_3, layout_ops_8_4, layout_ops_8_5, layout_ops_8_6;
+// one kernel table per (P, N, V) object of fmx_layout.hip
+extern const LayoutOps layout_ops_4_2_32, layout_ops_4_2_64, layout_ops_4_2_128, layout_ops_4_3_32, layout_ops_4_3_64,
+    layout_ops_4_3_128, layout_ops_4_4_32, layout_ops_4_4_64, layout_ops_4_4_128, layout_ops_4_5_32,
+    layout_ops_4_5_64, layout_ops_4_5_128, layout_ops_4_6_32, layout_ops_4_6_64, layout_ops_4_6_128,
+    layout_ops_8_2_32, layout_ops_8_2_64, layout_ops_8_2_128, layout_ops_8_3_32, layout_ops_8_3_64,
+    layout_ops_8_3_128, layout_ops_8_4_32, layout_ops_8_4_64, layout_ops_8_4_128, layout_ops_8_5_32,
+    layout_ops_8_5_64, layout_ops_8_5_128, layout_ops_8_6_32, layout_ops_8_6_64, layout_ops_8_6_128;
 
 // The layout's kernel table and the run-time part of its layout (V, record).
 struct Disp {
@@ -145,12 +150,21 @@ struct Disp {
     uint32_t vb, rec;
 };
 static Disp dispatch(const fmx_index *ix) {
-    static const LayoutOps *const tab[2][5] = {
-        {&layout_ops_4_2, &layout_ops_4_3, &layout_ops_4_4, &layout_ops_4_5, &layout_ops_4_6},
-        {&layout_ops_8_2, &layout_ops_8_3, &layout_ops_8_4, &layout_ops_8_5, &layout_ops_8_6}};
+    static const LayoutOps *const tab[2][5][3] = {
+        {{&layout_ops_4_2_32, &layout_ops_4_2_64, &layout_ops_4_2_128},
+         {&layout_ops_4_3_32, &layout_ops_4_3_64, &layout_ops_4_3_128},
+         {&layout_ops_4_4_32, &layout_ops_4_4_64, &layout_ops_4_4_128},
+         {&layout_ops_4_5_32, &layout_ops_4_5_64, &layout_ops_4_5_128},
+         {&layout_ops_4_6_32, &layout_ops_4_6_64, &layout_ops_4_6_128}},
+        {{&layout_ops_8_2_32, &layout_ops_8_2_64, &layout_ops_8_2_128},
+         {&layout_ops_8_3_32, &layout_ops_8_3_64, &layout_ops_8_3_128},
+         {&layout_ops_8_4_32, &layout_ops_8_4_64, &layout_ops_8_4_128},
+         {&layout_ops_8_5_32, &layout_ops_8_5_64, &layout_ops_8_5_128},
+         {&layout_ops_8_6_32, &layout_ops_8_6_64, &layout_ops_8_6_128}}};
     const fmx_layout &L = ix->bv.L;
     const uint32_t rec = ix->occ_mode == FMX_OCC_INTERLEAVED ? ix->rec_bytes : 0;
-    return Disp{tab[L.pos_bytes == 4 ? 0 : 1][L.planes - 2], L.vec_bits, rec};
+    const uint32_t vi = L.vec_bits == 32 ? 0 : L.vec_bits == 64 ? 1 : 2;
+    return Disp{tab[L.pos_bytes == 4 ? 0 : 1][L.planes - 2][vi], L.vec_bits, rec};
 }
 
 

@@ -243,24 +243,32 @@ int by_vb(uint32_t vb, uint32_t rec, const orc_index &ox, uint32_t options, cons
     return by_rec<P, N, 128>(rec, ox, options, b, o, n, f, c, l, cap, need);
 }
 
-template <typename P>
-int by_n(const orc_index &ox, uint32_t rec, uint32_t options, const uint8_t *b, const uint64_t *o, uint64_t n,
-         uint32_t f, uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need) {
-    switch (ox.L.planes) {
-        case 2: return by_vb<P, 2>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
-        case 3: return by_vb<P, 3>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
-        case 4: return by_vb<P, 4>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
-        case 5: return by_vb<P, 5>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
-        default: return by_vb<P, 6>(ox.L.vec_bits, rec, ox, options, b, o, n, f, c, l, cap, need);
-    }
-}
-
 }  // namespace
+
+// Built once per (P, N) pair (-DEMU_P=4|8 -DEMU_N=2..6, tests/emu/Makefile:
+// ten objects compiled in parallel) plus the dispatching object (no EMU_P).
+#define EMU_NAME2(p, n) emu_run_##p##_##n
+#define EMU_NAME(p, n) EMU_NAME2(p, n)
+#define EMU_ARGS                                                                                                   \
+    uint32_t vb, uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b, const uint64_t *o,        \
+        uint64_t n, uint32_t f, uint64_t *c, uint64_t *l, uint64_t cap, uint64_t *need
+
+#if defined(EMU_P)
+int EMU_NAME(EMU_P, EMU_N)(EMU_ARGS) {
+    using PT = std::conditional_t<EMU_P == 4, uint32_t, uint64_t>;
+    return by_vb<PT, EMU_N>(vb, rec, ox, options, b, o, n, f, c, l, cap, need);
+}
+#else
+int emu_run_4_2(EMU_ARGS); int emu_run_4_3(EMU_ARGS); int emu_run_4_4(EMU_ARGS); int emu_run_4_5(EMU_ARGS);
+int emu_run_4_6(EMU_ARGS); int emu_run_8_2(EMU_ARGS); int emu_run_8_3(EMU_ARGS); int emu_run_8_4(EMU_ARGS);
+int emu_run_8_5(EMU_ARGS); int emu_run_8_6(EMU_ARGS);
 
 extern "C" {
 
 // options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text,
-// 16 row contexts, 32 single-row deep-table entries; 64 here: plain records, neither paired-chunk nor symbol-mask); bits 8.. = the scan limit (FMX_SCAN_ROWS, 0 = default 32).
+// 16 row contexts, 32 single-row deep-table entries; 64 here: plain records,
+// neither paired-chunk nor symbol-mask); bits 8.. = the scan limit
+// (FMX_SCAN_ROWS, 0 = default 32).
 // Outputs are u64: counts[npat] and the concatenated locations.
 int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
                uint32_t encoder, uint32_t options, const uint8_t *bytes, const uint64_t *offs, uint64_t npat,
@@ -269,12 +277,18 @@ int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t p
     orc_index ox;
     int st = orc_load(blob, len, L, &ox, nullptr, nullptr);
     if (st) return st;
-    // the loader's record choice (k_relayout); options bit 64: plain records only
-    const uint32_t rec = (options & 1u) ? interleaved_rec_bytes(pos_bytes, planes, vec_bits, ox.sigma,
-                                                                (options & 64u) == 0, (options & 64u) == 0)
-                                        : 0u;
-    if (pos_bytes == 4) return by_n<uint32_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
-    return by_n<uint64_t>(ox, rec, options, bytes, offs, npat, flags, counts, locs, cap, needed);
+    // the loader's record choice (fmx_load / k_relayout): option bit 64 keeps
+    // plain records; multi-line symbol masks only without derived structures
+    const bool fancy = (options & 64u) == 0, multi = fancy && (options & 62u) == 0;
+    const uint32_t rec =
+        (options & 1u) ? interleaved_rec_bytes(pos_bytes, planes, vec_bits, ox.sigma, fancy, fancy, multi) : 0u;
+    using Run = int (*)(EMU_ARGS);
+    static const Run tab[2][5] = {{emu_run_4_2, emu_run_4_3, emu_run_4_4, emu_run_4_5, emu_run_4_6},
+                                  {emu_run_8_2, emu_run_8_3, emu_run_8_4, emu_run_8_5, emu_run_8_6}};
+    if (planes < 2 || planes > 6) return -1;
+    return tab[pos_bytes == 4 ? 0 : 1][planes - 2](vec_bits, rec, ox, options, bytes, offs, npat, flags, counts, locs,
+                                                   cap, needed);
 }
 
 }  // extern "C"
+#endif

@@ -25,7 +25,7 @@ OPTIONS = (0, 1, 1 | 64, 31 | 64, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 2 | 8, 31,
 
 @pytest.fixture(scope="module")
 def emu():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "emu")])
+    subprocess.check_call(["make", "-s", "-j", str(min(8, os.cpu_count() or 1)), "-C", os.path.join(HERE, "emu")])
     lib = C.CDLL(EMU)
     u32, u64, p = C.c_uint32, C.c_uint64, C.c_void_p
     lib.emu_locate.argtypes = [p, u64, u32, u32, u32, u32, u32, p, p, u64, u32, p, p, u64, C.POINTER(u64)]
