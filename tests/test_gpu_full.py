@@ -199,3 +199,45 @@ def test_builder_u32_limit(pkg, O, n):
     path), with u32 positions as close to 2^32 as they go (C[sigma] = n):
     2,000 patterns answered like the oracle, each finding its own start."""
     _big_text_case(pkg, O, n, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), (4, 3, 64), seed=13)
+
+
+@pytest.mark.parametrize("n_run", [1 << 20, 200_000_000, 2_000_000_000])
+def test_builder_single_symbol_run(pkg, n_run):
+    """The builder's worst case: a run of one symbol leaves every suffix of the
+    run unresolved for ~log2(n) prefix-doubling rounds.  Text = A^n_run C G:
+    the answers are known in closed form — count(A^k) = n_run - k + 1,
+    locate(A^k C) = [n_run - k], count(C G) = 1 — so the check needs no oracle
+    (which would need minutes for 200 M equal suffixes)."""
+    import time
+    import torch
+    dev = torch.device("cuda:0")
+    n = n_run + 2
+    d_text = torch.full((n,), ord("A"), dtype=torch.uint8, device=dev)
+    d_text[n_run] = ord("C")
+    d_text[n_run + 1] = ord("G")
+    table = pkg.text_encoders.EncodingTable.from_symbols(ACGTN)
+    block = pkg.blocks.Block3(pkg.Vector.U64)
+    b = (pkg.FmIndexBuilder(n, table.symbol_count(), table, pkg.u32, block)
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    size = b.blob_size()
+    d_blob = torch.empty(size, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    b.build_device(d_text.data_ptr(), d_blob.data_ptr(), size)
+    torch.cuda.synchronize()
+    progress(f"A^{n_run:,}CG: blob built in {time.perf_counter() - t0:.2f} s")
+    blob = d_blob.cpu().numpy()
+    del d_text, d_blob
+    torch.cuda.empty_cache()
+    for options in (pkg._native.FMX_OPT_DEFAULT, pkg._native.FMX_OCC_BLOB):
+        ix = pkg.FmIndex.load(blob, pkg.u32, block, table, options=options)
+        ks = [1, 2, 3, 4, 7, 20, 64, 1000]
+        cnt = ix.count_batch([b"A" * k for k in ks])
+        assert [int(x) for x in cnt] == [n_run - k + 1 for k in ks]
+        pats = [b"A" * k + b"C" for k in (1, 5, 33, 500)] + [b"CG", b"G", b"AACG", b"T", b"GA"]
+        off, locs = ix.locate_batch(pats)
+        want = [[n_run - k] for k in (1, 5, 33, 500)] + [[n_run], [n_run + 1], [n_run - 2], [], []]
+        got = [sorted(int(x) for x in locs[int(off[i]):int(off[i + 1])]) for i in range(len(pats))]
+        assert got == want, (options, got, want)
+        ix.close()
