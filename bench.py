@@ -116,7 +116,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--streams", type=int, default=2, help="launches in flight (HIP streams)")
     ap.add_argument("--batches", type=int, default=32, help="distinct batches cycled (weak-scaling configs)")
-    ap.add_argument("--group", type=int, default=8, help="batches per kernel launch (at most 8)")
+    ap.add_argument("--group", type=int, default=8, help="batches per kernel launch (at most 16)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment: each launch group's patterns arranged so that workgroup tile t (XCD t %% 8) "

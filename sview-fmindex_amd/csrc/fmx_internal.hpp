@@ -155,7 +155,7 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                          hipStream_t stream);
 // One batch of a locate launch; a launch runs up to kMaxGroup of them, each
 // with its own patterns, outputs and workspace (fmx_locate_group_async).
-constexpr uint32_t kMaxGroup = 8;
+constexpr uint32_t kMaxGroup = 16;
 struct LocateBatch {
     const uint8_t *bytes;
     const uint64_t *offs;

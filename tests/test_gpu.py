@@ -485,7 +485,7 @@ def test_locate_queue_many_launches_one_workspace(pkg, O):
 
 
 def test_locate_group_launch(pkg, O):
-    """fmx_locate_group_async: up to 8 batches per k_locate launch (more are
+    """fmx_locate_group_async: up to 16 batches per launch (more are
     split over launches), sizes from 0 to a few thousand, forward and
     reversed, each batch's outputs equal to the host API's; repeated so the
     workspaces' look-back epochs wrap; a shared workspace is rejected."""
@@ -496,7 +496,8 @@ def test_locate_group_launch(pkg, O):
     blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
     dev = torch.device("cuda:0")
-    sizes = [2500, 0, 1, 700, 256, 257, 3000, 40, 1999, 5, 1024]  # 11 batches: two launches
+    sizes = [2500, 0, 1, 700, 256, 257, 3000, 40, 1999, 5, 1024,
+             33, 600, 0, 77, 4096, 12, 300, 2, 900, 128]  # 21 batches: two launches
     bats, jobs = [], []
     for bi, n in enumerate(sizes):
         rev = bi % 3 == 2
