@@ -298,12 +298,27 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     }
     ix->occ_mode = FMX_OCC_BLOB;
     if (options & FMX_OCC_INTERLEAVED) {
-        // multi-line symbol masks only for the faithful index (no derived structures)
-        const uint32_t rec = interleaved_record_bytes(v, (options & ~FMX_OCC_INTERLEAVED) == 0);
+        // multi-line symbol masks only for the faithful index (no derived
+        // structures); if their records do not fit in HBM, the one-line
+        // encodings, and if those do not fit either, the blob layout
+        uint32_t rec = interleaved_record_bytes(v, (options & ~FMX_OCC_INTERLEAVED) == 0);
+        // (FMX_OCC_MAX_MB caps the records' HBM: the same fallback, testable)
+        const char *cap_env = getenv("FMX_OCC_MAX_MB");
+        const uint64_t cap = cap_env ? strtoull(cap_env, nullptr, 10) << 20 : ~0ull;
+        auto alloc = [&](uint32_t r) {
+            if (r == 0 || v.blocks_len * (r & ~15u) > cap) return false;
+            if (hipMalloc(&ix->d_occ, v.blocks_len * (r & ~15u)) == hipSuccess) return true;
+            (void)hipGetLastError();  // (clear the out-of-memory error)
+            ix->d_occ = nullptr;
+            return false;
+        };
+        if (!alloc(rec)) {
+            const uint32_t one = interleaved_record_bytes(v, false);
+            rec = one != rec && alloc(one) ? one : 0u;
+        }
         if (rec != 0) {
             ix->rec_bytes = rec;
             ix->occ_bytes = v.blocks_len * (rec & ~15u);
-            if (hipMalloc(&ix->d_occ, ix->occ_bytes) != hipSuccess) return FMX_E_DEVICE;
             q.occ = ix->d_occ;
             q.rec_bytes = rec;
             ix->occ_mode = FMX_OCC_INTERLEAVED;

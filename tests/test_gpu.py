@@ -172,6 +172,28 @@ def test_record_encodings(pkg, O, pb, planes, vb, monkeypatch):
                 check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1 | 2 | 4)
 
 
+def test_record_fallback_when_hbm_is_short(pkg, O, monkeypatch):
+    """fmx_load falls back from multi-line symbol masks to the one-line
+    encodings, then to the blob layout, when the records do not fit in HBM
+    (FMX_OCC_MAX_MB stands in for a full device); answers are unchanged."""
+    rng = np.random.default_rng(21)
+    chars = rand_chr_list(rng, 21)
+    table = table_from_symbols([bytes([c]) for c in chars])
+    text = rand_text(rng, chars, 300_000, 300_000)
+    blob = gpu_build(pkg, text, 21, 4, 5, 64, 3, 2, table)
+    pats = [rand_pattern(rng, text, 1, 14) for _ in range(500)]
+    blocks = len(text) // 64 + 1
+    for cap_mb, want in ((None, 384 | 2), ((blocks * 128 >> 20) + 1, 128), (0, 0)):
+        if cap_mb is None:
+            monkeypatch.delenv("FMX_OCC_MAX_MB", raising=False)
+        else:
+            monkeypatch.setenv("FMX_OCC_MAX_MB", str(cap_mb))
+        ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block5(pkg.Vector.U64), options=1)
+        assert ix.info()["occ_record"] == want, (cap_mb, ix.info()["occ_record"])
+        ix.close()
+        check_parity(pkg, O, blob, 4, 5, 64, 0, pats, 1, reversed_too=False)
+
+
 @pytest.mark.parametrize("n", [0, 1, 31, 32, 33, 64, 127, 128, 129, 4096])
 def test_block_boundaries(pkg, O, n):
     """n % BLOCK_LEN == 0 appends a zero block + checkpoint row (bwm/mod.rs:136-142)."""
