@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 3u
+#define FMX_ABI_VERSION 4u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -113,6 +113,11 @@ typedef struct fmx_layout {
  * load time, paid back only after ~10^10 patterns (bench.py "derived"). */
 #define FMX_OPT_DERIVED (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | \
                          FMX_OPT_ROW_CONTEXT | FMX_OPT_LUT_ROWS)
+/* fmx_load_file only: read the blob's body with O_DIRECT, bypassing the page
+ * cache — a cold load from storage, what the reference bench measures after
+ * dropping the caches (bench/run_benchmark.sh:53-56).  FMX_E_ARG if the
+ * file system refuses O_DIRECT (tmpfs does). */
+#define FMX_LOAD_DIRECT (1u << 16)
 
 typedef struct fmx_index fmx_index; /* opaque; one per (blob, device) */
 
@@ -161,7 +166,10 @@ fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, i
 
 /* Same, for a blob already resident in HBM of `device` (e.g. written by
  * fmx_build_device).  The device blob is borrowed and must outlive the index.
- * Starts after all work already queued on the device (it synchronises). */
+ * Starts after all work already queued on the device: it calls
+ * hipDeviceSynchronize, which also waits for unrelated work on other streams
+ * (other threads' queries, pending collectives) — load before serving starts,
+ * or order the blob's writer yourself and accept that wait once. */
 fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout layout, int device,
                            uint32_t options, fmx_index **out, uint64_t *expected_total,
                            uint64_t *actual_total);
@@ -213,11 +221,8 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
  * [256 B][tile counts][tile offsets][one search record per pattern].  A
  * workspace is zeroed by the caller before its first use, then belongs to
- * this index: its launches are ordered on one stream at a time.  (The
- * default locate is k_search + k_emit, which never makes one workgroup wait
- * on another; with FMX_LOCATE_FUSED=1 in the environment the single-kernel
- * k_locate is used instead, and the index tracks a look-back epoch per
- * workspace address and clears what it needs.) */
+ * this index: its launches are ordered on one stream at a time.  (A locate is
+ * k_search + k_emit, neither of which makes one workgroup wait on another.) */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)
@@ -261,11 +266,23 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
 /* Wait for `stream` and return (and clear) the latched device status. */
 fmx_status fmx_sync(fmx_index *ix, void *stream);
 
+/* The caller is done with `stream` (e.g. before hipStreamDestroy): wait for it,
+ * return (and clear) its latched status like fmx_sync, and free its status
+ * word for reuse.  Optional: an index holds 1024 status words and recycles
+ * the least recently used one whose stream has no launch in flight, so a
+ * caller that makes a stream per request never runs out; bits latched on a
+ * recycled word and never read are dropped.  A destroyed stream's handle may
+ * be reused by a new stream, which then shares the old status word — release
+ * (or sync) a stream before destroying it. */
+fmx_status fmx_stream_release(fmx_index *ix, void *stream);
+
 /* --------------------------------------------------------------- timing
  * enable = k > 0: every k-th kernel launch (k = 1: every launch) is bracketed
  * by hipEvents on its stream; 0: off.  fmx_timing_read sums the bracketed
  * durations per kernel (it synchronises).  An event pair costs the stream
- * several microseconds, so throughput runs sample (k > 1). */
+ * several microseconds, so throughput runs sample (k > 1).  Timers: "count",
+ * "locate" (a whole locate launch) and, for fmx_locate_group_async, its two
+ * kernels "locate.search" (k_search) and "locate.emit" (k_emit). */
 fmx_status fmx_timing_enable(fmx_index *ix, int enable);
 fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entries, int *n_entries);
 

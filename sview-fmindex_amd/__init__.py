@@ -421,17 +421,22 @@ class FmIndex:
     def load_file(cls, path, position: Position = u32, block: Optional[_Block] = None,
                   text_encoder=text_encoders.EncodingTable, device: int = 0, occ: str = "interleaved",
                   deep_lut: bool = False, full_sa: bool = False, text: bool = False, context: bool = False,
-                  lut_rows: bool = False, options: Optional[int] = None, chunk_bytes: int = 0) -> "FmIndex":
+                  lut_rows: bool = False, options: Optional[int] = None, chunk_bytes: int = 0,
+                  direct: bool = False) -> "FmIndex":
         """Blob file -> HBM (fmx_load_file): what the bench's mmap loader
         (bench/src/locate/sview_mmap.rs:17-45) followed by ``FmIndex::load``
         does, as a streamed ingest — the header is validated from the file,
-        then the body is read in pinned chunks overlapped with their DMA."""
+        then the body is read in pinned chunks overlapped with their DMA.
+        `direct`: the body is read with O_DIRECT (FMX_LOAD_DIRECT), bypassing
+        the page cache — a cold load (raises if the file system refuses it)."""
         block = block or blocks.Block2(Vector.U64)
         if isinstance(text_encoder, type):
             text_encoder = text_encoder.__new__(text_encoder)
         h = C.c_void_p()
         exp, act = C.c_uint64(), C.c_uint64()
         mode = options if options is not None else _options(occ, deep_lut, full_sa, text, context, lut_rows)
+        if direct:
+            mode |= _n.FMX_LOAD_DIRECT
         st = _n.lib().fmx_load_file(os.fsencode(path), _layout(position, block, text_encoder), device, mode,
                                     int(chunk_bytes), C.byref(h), C.byref(exp), C.byref(act))
         if st == _n.FMX_E_FORMAT:
@@ -592,6 +597,11 @@ class FmIndex:
 
     def sync(self, stream: int = 0) -> None:
         _check(_n.lib().fmx_sync(self._h, C.c_void_p(stream) if stream else None))
+
+    def release_stream(self, stream: int) -> None:
+        """Done with `stream`: wait for it, raise what it latched (as sync),
+        free its status word (fmx_stream_release)."""
+        _check(_n.lib().fmx_stream_release(self._h, C.c_void_p(stream) if stream else None))
 
     def timing_enable(self, on: bool = True, every: int = 1) -> None:
         """Bracket every `every`-th launch with HIP events (fmx_timing_enable)."""

@@ -38,6 +38,7 @@ FMX_OPT_LUT_ROWS = 32
 FMX_OPT_DEFAULT = FMX_OCC_INTERLEAVED
 FMX_OPT_DERIVED = (FMX_OCC_INTERLEAVED | FMX_OPT_DEEP_LUT | FMX_OPT_FULL_SA | FMX_OPT_TEXT | FMX_OPT_ROW_CONTEXT
                    | FMX_OPT_LUT_ROWS)
+FMX_LOAD_DIRECT = 1 << 16
 
 
 class fmx_layout(C.Structure):
@@ -90,6 +91,7 @@ SIGNATURES = {
     "fmx_locate_jobs_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64]),
     "fmx_locate_group_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64, _p]),
     "fmx_sync": (_i, [_p, _p]),
+    "fmx_stream_release": (_i, [_p, _p]),
     "fmx_timing_enable": (_i, [_p, _i]),
     "fmx_timing_read": (_i, [_p, C.POINTER(fmx_kernel_timing), _i, C.POINTER(_i)]),
     "fmx_build_blob_size": (_i, [_u64, _u32, fmx_layout, _u32, _u32, _PU64]),

@@ -207,9 +207,28 @@ static hipError_t timed(fmx_index *ix, const char *name, hipStream_t s, uint64_t
     hipEventRecord(a, s);
     hipError_t e = launch();
     hipEventRecord(b, s);
-    Timer &t = timer(ix, name);
-    t.pending.emplace_back(a, b);
-    t.pending_units.push_back(units);
+    timer(ix, name).pending.push_back(TimedSpan{a, b, true, true, units});
+    return e;
+}
+
+// The same for a locate launch, with a third event between its two kernels:
+// timers `name` (the launch), `first` (k_search) and `second` (k_emit).
+template <class F>
+static hipError_t timed_split(fmx_index *ix, const char *name, const char *first, const char *second, hipStream_t s,
+                              uint64_t units, F &&launch) {
+    std::unique_lock<std::mutex> g(ix->timing_mu);
+    if (!ix->timing || (ix->timing_seq++ % ix->timing_every) != 0) {
+        g.unlock();
+        return launch(nullptr);
+    }
+    hipEvent_t a = take_event(ix), m = take_event(ix), b = take_event(ix);
+    if (!a || !m || !b) return hipErrorOutOfMemory;
+    hipEventRecord(a, s);
+    hipError_t e = launch(m);
+    hipEventRecord(b, s);
+    timer(ix, name).pending.push_back(TimedSpan{a, b, true, true, units});
+    timer(ix, first).pending.push_back(TimedSpan{a, m, false, true, units});
+    timer(ix, second).pending.push_back(TimedSpan{m, b, false, false, units});
     return e;
 }
 
@@ -244,15 +263,80 @@ struct LoadTrace {
 
 // The status word of `s`: every stream an index launches on gets a device
 // word of its own, so fmx_sync(s) reads and clears only what that stream's
-// launches latched (stream-ordered), never another stream's.
-static uint32_t *status_slot(fmx_index *ix, hipStream_t s) {
-    std::lock_guard<std::mutex> g(ix->status_mu);
+// launches latched (stream-ordered), never another stream's.  A stream seen
+// for the first time takes a free slot, or else the least recently used slot
+// whose launches have all completed (its `done` event): the slot changes
+// owner and its word is zeroed on the new stream before that stream's first
+// launch, so bits an earlier owner latched and never read are dropped
+// (fmx_sync or fmx_stream_release collect them).  Only when every slot's
+// stream still has launches in flight is there no slot (FMX_E_DEVICE).
+// `launch`: the slot is held (not recycled) until status_launched() records
+// the launch's completion event.  Caller holds status_mu.
+static int status_slot_locked(fmx_index *ix, hipStream_t s, bool launch) {
     auto it = ix->status_of.find((const void *)s);
-    if (it != ix->status_of.end()) return it->second;
-    if (ix->status_used >= kStatusSlots) return nullptr;
-    uint32_t *w = ix->d_status + ix->status_used++;
-    ix->status_of.emplace((const void *)s, w);
-    return w;
+    if (it != ix->status_of.end()) {
+        StatusSlot &sl = ix->slots[it->second];
+        sl.last = ++ix->status_clock;
+        sl.inflight += launch ? 1u : 0u;
+        return (int)it->second;
+    }
+    if (!launch) return -1;  // (a stream that never launched has nothing latched)
+    int idx = -1;
+    if (!ix->free_slots.empty()) {
+        idx = (int)ix->free_slots.back();
+        ix->free_slots.pop_back();
+    } else {
+        uint64_t best = ~0ull;
+        for (uint32_t i = 0; i < ix->slots.size(); ++i) {
+            const StatusSlot &sl = ix->slots[i];
+            if (sl.pinned || sl.inflight || sl.last >= best) continue;
+            if (sl.launched && hipEventQuery(sl.done) != hipSuccess) continue;
+            best = sl.last;
+            idx = (int)i;
+        }
+        if (idx < 0) return -1;
+        ix->status_of.erase(ix->slots[idx].key);
+    }
+    StatusSlot &sl = ix->slots[idx];
+    if (hipMemsetAsync(ix->d_status + idx, 0, 4, s) != hipSuccess) {
+        sl.key = nullptr;
+        ix->free_slots.push_back((uint32_t)idx);
+        return -1;
+    }
+    sl.key = (const void *)s;
+    sl.last = ++ix->status_clock;
+    sl.inflight = 1;
+    sl.launched = false;
+    ix->status_of.emplace((const void *)s, (uint32_t)idx);
+    return idx;
+}
+
+static uint32_t *status_slot(fmx_index *ix, hipStream_t s, int *idx) {
+    std::lock_guard<std::mutex> g(ix->status_mu);
+    *idx = status_slot_locked(ix, s, true);
+    return *idx < 0 ? nullptr : ix->d_status + *idx;
+}
+
+// After the launch(es) of a status_slot() call were queued on s: record the
+// slot's completion event and release the hold.
+static void status_launched(fmx_index *ix, int idx, hipStream_t s) {
+    std::lock_guard<std::mutex> g(ix->status_mu);
+    StatusSlot &sl = ix->slots[idx];
+    if (!sl.done && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) sl.done = nullptr;
+    if (sl.done && hipEventRecord(sl.done, s) == hipSuccess) sl.launched = true;
+    else if (!sl.done) sl.pinned = true;  // (cannot tell when it completes: never recycle it)
+    if (sl.inflight) --sl.inflight;
+}
+
+// status_slot + status_launched around one launch function.
+template <class F>
+static fmx_status with_status(fmx_index *ix, hipStream_t s, F &&launch) {
+    int idx = -1;
+    uint32_t *status = status_slot(ix, s, &idx);
+    if (!status) return FMX_E_DEVICE;
+    const fmx_status st = launch(status);
+    status_launched(ix, idx, s);
+    return st;
 }
 
 static fmx_status ensure_scratch(fmx_index *ix, uint64_t bytes) {
@@ -290,7 +374,15 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     if (hipMemset(ix->d_status, 0, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
-    q.status = status_slot(ix, ix->stream);
+    ix->slots.assign(kStatusSlots, StatusSlot{});
+    for (uint32_t i = kStatusSlots; i-- > 0;) ix->free_slots.push_back(i);
+    {
+        int idx = -1;
+        q.status = status_slot(ix, ix->stream, &idx);
+        if (!q.status) return FMX_E_DEVICE;
+        ix->slots[idx].pinned = true;
+        ix->slots[idx].inflight = 0;
+    }
     // the k-mer count table (W^k entries of P) goes to LDS when it is small
     {
         const uint64_t ktb = v.kmer_len * v.L.pos_bytes;
@@ -404,8 +496,13 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
 }
 
 static fmx_status read_status(fmx_index *ix, hipStream_t s) {
-    uint32_t *w = status_slot(ix, s);
-    if (!w) return FMX_E_DEVICE;
+    int idx;
+    {
+        std::lock_guard<std::mutex> g(ix->status_mu);
+        idx = status_slot_locked(ix, s, false);
+    }
+    if (idx < 0) return dev_err(hipStreamSynchronize(s));  // never launched on: nothing latched
+    uint32_t *w = ix->d_status + idx;
     uint32_t st = 0;
     if (hipMemcpyAsync(&st, w, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
     if (hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
@@ -538,10 +635,27 @@ static bool read_full(int fd, uint64_t off, uint64_t len, void *dst) {
     return true;
 }
 
+// O_DIRECT read of [off, off + len): off and dst are 4 KiB aligned; the
+// request is rounded up to whole 4 KiB blocks (the file's end makes the last
+// one short), so dst must have room for the rounded length.
+static bool read_direct(int fd, uint64_t off, uint64_t len, void *dst) {
+    uint8_t *d = (uint8_t *)dst;
+    uint64_t want = align_up(len, 4096), got = 0;
+    while (got < len) {
+        const uint64_t ask = std::min<uint64_t>(want - got, 1ull << 30);
+        const ssize_t r = pread(fd, d + got, ask, (off_t)(off + got));
+        if (r <= 0) return false;
+        got += (uint64_t)r;
+        if ((uint64_t)r < ask && got < len && (got & 4095)) return false;  // short, unaligned: cannot go on
+    }
+    return true;
+}
+
 // File -> HBM through a ring of pinned chunks: each chunk is read by
 // kReadThreads threads (page-cache copies run ~5-10 GB/s per thread) while
-// earlier chunks are in flight to the device on one stream.
-static fmx_status stream_file(int fd, uint64_t len, uint8_t *d_dst, uint64_t chunk) {
+// earlier chunks are in flight to the device on one stream.  direct: fd was
+// opened with O_DIRECT (reads bypass the page cache: a cold load).
+static fmx_status stream_file(int fd, uint64_t len, uint8_t *d_dst, uint64_t chunk, bool direct) {
     constexpr int kBufs = 4, kReadThreads = 8;
     hipStream_t s = nullptr;
     void *buf[kBufs] = {};
@@ -562,17 +676,22 @@ static fmx_status stream_file(int fd, uint64_t len, uint8_t *d_dst, uint64_t chu
         const uint64_t slice = std::max<uint64_t>(align_up((n + kReadThreads - 1) / kReadThreads, 4096), 4ull << 20);
         std::vector<std::thread> th;
         std::atomic<bool> ok{true};
+        auto rd = [&](uint64_t o) {
+            const uint64_t l = std::min(slice, n - o);
+            return direct ? read_direct(fd, off + o, l, (uint8_t *)buf[b] + o)
+                          : read_full(fd, off + o, l, (uint8_t *)buf[b] + o);
+        };
         uint64_t o = slice;
         try {  // (no exception may leave the C ABI)
             for (; o < n; o += slice)
                 th.emplace_back([&, o] {
-                    if (!read_full(fd, off + o, std::min(slice, n - o), (uint8_t *)buf[b] + o)) ok = false;
+                    if (!rd(o)) ok = false;
                 });
         } catch (...) {  // no more threads: this one reads the rest
             for (; o < n; o += slice)
-                if (!read_full(fd, off + o, std::min(slice, n - o), (uint8_t *)buf[b] + o)) ok = false;
+                if (!rd(o)) ok = false;
         }
-        if (!read_full(fd, off, std::min(slice, n), buf[b])) ok = false;
+        if (!rd(0)) ok = false;
         for (auto &t : th) t.join();
         if (!ok) { st = FMX_E_ARG; break; }
         if (hipMemcpyAsync(d_dst + off, buf[b], n, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -593,8 +712,16 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
     if (!out || !path) return FMX_E_ARG;
     *out = nullptr;
     if (!layout_valid(layout)) return FMX_E_LAYOUT;
+    const bool direct = (options & FMX_LOAD_DIRECT) != 0;
+    options &= ~FMX_LOAD_DIRECT;
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return FMX_E_ARG;
+    int dfd = -1;  // the body's reads bypass the page cache (the header's go through it)
+    if (direct && (dfd = open(path, O_RDONLY | O_CLOEXEC | O_DIRECT)) < 0) { close(fd); return FMX_E_ARG; }
+    auto close_all = [&] {
+        close(fd);
+        if (dfd >= 0) close(dfd);
+    };
     struct stat sb;
     if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close(fd); return FMX_E_ARG; }
     const uint64_t blob_len = (uint64_t)sb.st_size;
@@ -604,27 +731,27 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
         return off + len <= blob_len && read_full(fd, off, len, dst);
     };
     fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
-    if (st) { close(fd); return st; }
+    if (st) { close_all(); return st; }
     tr.mark("parse headers");
     DeviceGuard dg(device);
-    if (!dg.ok) { close(fd); return FMX_E_DEVICE; }
+    if (!dg.ok) { close_all(); return FMX_E_DEVICE; }
     tr.mark("device (first HIP call)");
     fmx_index *ix = new (std::nothrow) fmx_index();
-    if (!ix) { close(fd); return FMX_E_DEVICE; }
+    if (!ix) { close_all(); return FMX_E_DEVICE; }
     ix->bv = bv;
     ix->device = device;
     ix->blob_len = blob_len;
     if (hipMalloc(&ix->d_blob_owned, std::max<uint64_t>(blob_len, 1)) != hipSuccess) {
-        close(fd);
+        close_all();
         fmx_free(ix);
         return FMX_E_DEVICE;
     }
     tr.mark("hipMalloc blob");
     const uint64_t chunk = chunk_bytes ? align_up(chunk_bytes, 4096) : (16ull << 20);
-    st = stream_file(fd, blob_len, ix->d_blob_owned, chunk);
-    close(fd);
+    st = stream_file(direct ? dfd : fd, blob_len, ix->d_blob_owned, chunk, direct);
+    close_all();
     if (st) { fmx_free(ix); return st; }
-    tr.mark("file -> HBM");
+    tr.mark(direct ? "file -> HBM (O_DIRECT)" : "file -> HBM");
     ix->d_blob = ix->d_blob_owned;
     st = finish_load(ix, options);
     if (st) { fmx_free(ix); return st; }
@@ -638,8 +765,13 @@ void fmx_free(fmx_index *ix) {
     DeviceGuard dg(ix->device);
     if (ix->stream) hipStreamSynchronize(ix->stream);
     for (auto &t : ix->timers)
-        for (auto &p : t.pending) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+        for (auto &p : t.pending) {
+            if (p.own_a) hipEventDestroy(p.a);
+            if (p.own_b) hipEventDestroy(p.b);
+        }
     for (auto e : ix->event_pool) hipEventDestroy(e);
+    for (auto &sl : ix->slots)
+        if (sl.done) hipEventDestroy(sl.done);
     if (ix->d_scratch) hipFree(ix->d_scratch);
     if (ix->d_ws) hipFree(ix->d_ws);
     if (ix->d_occ) hipFree(ix->d_occ);
@@ -685,12 +817,12 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
                                  uint32_t flags, void *d_counts, void *stream) {
     if (!ix || (n && (!d_bytes || !d_offsets || !d_counts))) return FMX_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
-    uint32_t *status = status_slot(ix, s);
-    if (!status) return FMX_E_DEVICE;
     DeviceGuard dg(ix->device);
-    return dev_err(timed(ix, "count", s, n, [&] {
-        return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, status, s);
-    }));
+    return with_status(ix, s, [&](uint32_t *status) {
+        return dev_err(timed(ix, "count", s, n, [&] {
+            return launch_count(ix, d_bytes, d_offsets, n, flags, d_counts, status, s);
+        }));
+    });
 }
 
 // Locate workspace: [256 B reserved][tile counts: G][tile offsets: G]
@@ -718,14 +850,14 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
         return dev_err(e);
     }
     if (ws_bytes < ws_bytes_for(ix, n)) return FMX_E_ARG;
-    uint32_t *status = status_slot(ix, s);
-    if (!status) return FMX_E_DEVICE;
     uint8_t *ws = (uint8_t *)d_ws;
     const uint64_t G = locate_tiles_cap(n);
-    return dev_err(timed(ix, "locate", s, n, [&] {
-        return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
-                             (uint64_t *)(ws + 256), G, status, s);
-    }));
+    return with_status(ix, s, [&](uint32_t *status) {
+        return dev_err(timed(ix, "locate", s, n, [&] {
+            return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
+                                 (uint64_t *)(ws + 256), G, status, s);
+        }));
+    });
 }
 
 fmx_status fmx_locate_jobs_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs) {
@@ -752,9 +884,8 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
         for (uint64_t k = 0; k < i; ++k)
             if (jobs[k].d_workspace == j.d_workspace) return FMX_E_ARG;  // the batches run concurrently
     }
-    uint32_t *status = status_slot(ix, s);
-    if (!status) return FMX_E_DEVICE;
     DeviceGuard dg(ix->device);
+    return with_status(ix, s, [&](uint32_t *status) -> fmx_status {
     // up to kMaxGroup non-empty batches per launch; empty ones get their
     // zero offset and total directly
     uint64_t i = 0;
@@ -783,18 +914,36 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
             stage |= j.flags & FMX_HINT_LONG_PATTERNS;
         }
         if (grp.n == 0) continue;
-        const fmx_status st = dev_err(timed(ix, "locate", s, units, [&] {
-            return launch_locate_group(ix, grp, stage, status, s);
+        const fmx_status st = dev_err(timed_split(ix, "locate", "locate.search", "locate.emit", s, units,
+                                                  [&](hipEvent_t mid) {
+            return launch_locate_group(ix, grp, stage, status, s, mid);
         }));
         if (st) return st;
     }
     return FMX_OK;
+    });
 }
 
 fmx_status fmx_sync(fmx_index *ix, void *stream) {
     if (!ix) return FMX_E_ARG;
     DeviceGuard dg(ix->device);
     return read_status(ix, stream ? (hipStream_t)stream : ix->stream);
+}
+
+fmx_status fmx_stream_release(fmx_index *ix, void *stream) {
+    if (!ix) return FMX_E_ARG;
+    DeviceGuard dg(ix->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    const fmx_status st = read_status(ix, s);
+    std::lock_guard<std::mutex> g(ix->status_mu);
+    auto it = ix->status_of.find((const void *)s);
+    if (it != ix->status_of.end() && !ix->slots[it->second].pinned && ix->slots[it->second].inflight == 0) {
+        ix->slots[it->second].key = nullptr;
+        ix->slots[it->second].launched = false;
+        ix->free_slots.push_back(it->second);
+        ix->status_of.erase(it);
+    }
+    return st;
 }
 
 // ----------------------------------------------------------- host buffers
@@ -932,19 +1081,21 @@ fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entrie
     if (!ix || !n_entries) return FMX_E_ARG;
     std::lock_guard<std::mutex> g(ix->timing_mu);
     for (auto &t : ix->timers) {
-        for (size_t i = 0; i < t.pending.size(); ++i) {
-            auto &p = t.pending[i];
-            if (hipEventSynchronize(p.second) != hipSuccess) return FMX_E_DEVICE;
+        for (const TimedSpan &p : t.pending) {
+            if (hipEventSynchronize(p.b) != hipSuccess) return FMX_E_DEVICE;
             float ms = 0.f;
-            hipEventElapsedTime(&ms, p.first, p.second);
+            hipEventElapsedTime(&ms, p.a, p.b);
             t.ms += ms;
             t.launches += 1;
-            t.units += t.pending_units[i];
-            ix->event_pool.push_back(p.first);
-            ix->event_pool.push_back(p.second);
+            t.units += p.units;
+        }
+    }
+    for (auto &t : ix->timers) {  // (events go back to the pool once every timer has read them)
+        for (const TimedSpan &p : t.pending) {
+            if (p.own_a) ix->event_pool.push_back(p.a);
+            if (p.own_b) ix->event_pool.push_back(p.b);
         }
         t.pending.clear();
-        t.pending_units.clear();
     }
     int k = 0;
     for (auto &t : ix->timers) {

@@ -93,13 +93,33 @@ constexpr uint32_t kStatusEmpty = 1u;
 constexpr uint32_t kStatusSymbol = 2u;
 constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
 
+// One bracketed launch of a timer: events a -> b; own_a / own_b say whether
+// this entry returns the event to the pool when read (a split launch's
+// "search" and "emit" timers share their events with its "locate" timer).
+struct TimedSpan {
+    hipEvent_t a, b;
+    bool own_a, own_b;
+    uint64_t units;
+};
+
 struct Timer {
     std::string name;
     uint64_t launches = 0;
     double ms = 0.0;
     uint64_t units = 0;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
-    std::vector<uint64_t> pending_units;
+    std::vector<TimedSpan> pending;
+};
+
+// A status word's owner: the stream it is assigned to, the event recorded
+// after that stream's latest launch (a slot is recycled only once it has
+// completed), and its recency for least-recently-used recycling.
+struct StatusSlot {
+    const void *key = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t last = 0;
+    uint32_t inflight = 0;  // assigned to a launch that has not recorded `done` yet
+    bool launched = false;
+    bool pinned = false;    // the index's own stream: never recycled
 };
 
 }  // namespace fmx
@@ -117,8 +137,10 @@ struct fmx_index {
     uint32_t occ_mode = FMX_OCC_BLOB;
     uint32_t rec_bytes = 0;
     uint32_t *d_status = nullptr;  // kStatusSlots words: one per stream launched on
-    std::unordered_map<const void *, uint32_t *> status_of;
-    uint32_t status_used = 0;
+    std::vector<fmx::StatusSlot> slots;                   // kStatusSlots
+    std::unordered_map<const void *, uint32_t> status_of;  // stream -> slot
+    std::vector<uint32_t> free_slots;
+    uint64_t status_clock = 0;
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -174,8 +196,9 @@ struct LocateGroup {
     uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
     uint32_t n;
 };
+// `mid` (optional): an event recorded between k_search and k_emit (timing).
 hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
-                               uint32_t *status, hipStream_t stream);
+                               uint32_t *status, hipStream_t stream, hipEvent_t mid = nullptr);
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;

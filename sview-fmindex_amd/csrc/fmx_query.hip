@@ -198,10 +198,11 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
 
 // The kernels of a (grouped) locate, one after another on `stream`.
 static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp, uint32_t tiles,
-                               uint32_t sb, hipStream_t stream) {
+                               uint32_t sb, hipStream_t stream, hipEvent_t mid = nullptr) {
     const Disp d = dispatch(ix);
     hipError_t e = d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
+    if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     uint32_t fold = 1;
     for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
     if (!fold) {
@@ -227,7 +228,7 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
 }
 
 hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
-                               uint32_t *status, hipStream_t stream) {
+                               uint32_t *status, hipStream_t stream, hipEvent_t mid) {
     QueryArgs qa = ix->qa;
     qa.status = status;
     if (grp.n == 0 || grp.n > kMaxGroup || grp.tile_begin[0] != 0) return hipErrorInvalidValue;
@@ -237,7 +238,7 @@ hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint
         tiles += (grp.b[j].npat + 255) / 256;
     }
     if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    return launch_split(ix, qa, grp, (uint32_t)tiles, stage_bytes_for(stage_flags), stream);
+    return launch_split(ix, qa, grp, (uint32_t)tiles, stage_bytes_for(stage_flags), stream, mid);
 }
 
 uint64_t locate_rec_bytes(uint32_t pos_bytes) {

@@ -1,11 +1,22 @@
 """Multi-GPU helpers: one process per GPU, patterns sharded, blob replicated.
 
-Pattern batches are independent: rank r takes a contiguous
-slab of the global batch, runs it on its own GPU against its own replica of
-the blob, and the per-rank results are concatenated with all-gathers (RCCL
-over xGMI on MI355X nodes, gloo on CPU for tests).  No collective runs inside
-the query path itself; the gather of one launch's results can run on a
-communication stream while the next launch computes (`ShardGather`).
+Pattern batches are independent: every rank answers its
+share of a job against its own replica of the blob, and the per-rank results
+are concatenated with all-gathers (RCCL over xGMI on MI355X nodes, gloo on
+CPU for tests).  No collective runs inside the query path itself.
+
+- `JobPlan` deals a job of `total` patterns out: rank r takes the contiguous
+  slab `shard(total, world, r)`, cut into `nb` near-equal batches — `nb` the
+  same on every rank and a multiple of the launch-group size — so every rank
+  runs the same launches and per-rank pattern counts differ by at most one.
+- `JobGather` collects a sharded job's results with ONE all-gather per launch
+  group: each rank's counts and locations of the group's batches are packed
+  into one slab (counts first, then the locations of every batch back to
+  back), sized exactly from the batches' location totals, so the kernels
+  write their outputs straight into the slab and nothing is padded beyond
+  the largest rank's share.  `assemble()` concatenates the gathered slabs on
+  the device into the job's flat (offsets, locations) — the answer one
+  device would give for the whole job — with no host round trip per slot.
 """
 from __future__ import annotations
 
@@ -26,54 +37,141 @@ def shard_sizes(n_total: int, world: int) -> List[int]:
     return [e - s for s, e in (shard(n_total, world, r) for r in range(world))]
 
 
-class SlabGather:
-    """All-gather of per-rank locate results with no host round trip.
+class JobPlan:
+    """How a job of `total` patterns runs on `world` ranks in launch groups of
+    `group` batches of about `batch_target` patterns.
 
-    Each rank owns `slots` result slots of fixed shape: `batch` counts (P-wide)
-    and `loc_cap` locations — the kernels write a batch's counts and
-    locations straight into a slot (`counts_slot(j)`, `locs_slot(j)`), and
-    loc_cap is a bound every batch's total stays under (checked when the batch
-    first runs).  Everything is fixed-size, so `gather()` is two all-gathers
-    with no size exchange, enqueued on the current stream (issue it on a
-    communication stream to overlap it with the next launch).  `result(r, j,
-    n)` reads back slot j of rank r's first n patterns as (offsets,
-    locations) on the device."""
+    Rank r owns the global patterns shard(total, world, r); its slab is cut
+    into `nb` batches with shard(slab, nb, j) (sizes differ by at most one),
+    where nb = group * ceil(ceil(max slab / batch_target) / group) is the same
+    on every rank.  So every rank issues nb / group launches of about the
+    same size, and the ranks' pattern counts differ by at most one — the
+    round-robin deal of fixed 100 k batches it replaces gave 8-GPU C5 a 2:1
+    imbalance (10 batches over 8 ranks)."""
 
-    def __init__(self, world: int, slots: int, batch: int, loc_cap: int, count_dtype, loc_dtype, device,
-                 group=None):
+    def __init__(self, total: int, world: int, batch_target: int, group: int):
+        if total < 0 or world < 1 or batch_target < 1 or group < 1:
+            raise ValueError("JobPlan: total >= 0, world >= 1, batch_target >= 1, group >= 1")
+        self.total, self.world, self.group = int(total), int(world), int(group)
+        slab_max = -(-self.total // self.world)
+        per = max(1, -(-slab_max // int(batch_target)))
+        self.nb = -(-per // self.group) * self.group
+        self.spans = [shard(self.total, self.world, r) for r in range(self.world)]
+
+    @property
+    def groups(self) -> int:
+        return self.nb // self.group
+
+    def batches(self, rank: int) -> List[Tuple[int, int]]:
+        """Global pattern ranges [start, end) of rank's nb batches, in order."""
+        s, e = self.spans[rank]
+        return [(s + a, s + b) for a, b in (shard(e - s, self.nb, j) for j in range(self.nb))]
+
+    def sizes(self) -> np.ndarray:
+        """Patterns per batch, int64[world, nb]."""
+        return np.array([[b - a for a, b in self.batches(r)] for r in range(self.world)], dtype=np.int64)
+
+    def max_batch(self) -> int:
+        return int(self.sizes().max()) if self.total else 0
+
+
+class JobGather:
+    """One all-gather per launch group of a sharded job's results, into
+    exact-size slabs, assembled on the device.
+
+    `sizes[r][j]` / `needs[r][j]`: patterns / locations of rank r's batch j
+    (needs come from a sizing pass — bench.py's warm-up — exchanged once with
+    `all_gather_ints`).  Group g holds batches [g*group, (g+1)*group).  Rank
+    r's part of group g's slab is [its counts of those batches, in order]
+    [their locations, back to back]; every rank's part is padded to the
+    largest one, so the gather is one all_gather_into_tensor with no size
+    exchange in the loop.  `counts_slot(j)` / `locs_slot(j)` are the views the
+    kernels write batch j's counts and locations into (locations capacity =
+    needs[rank][j] exactly)."""
+
+    def __init__(self, sizes, needs, group: int, rank: int, dtype, device, pg=None):
         import torch
-        self.world, self.slots, self.batch, self.loc_cap = world, slots, batch, int(loc_cap)
-        self.group = group
-        self.counts_in = torch.zeros(slots * batch, dtype=count_dtype, device=device)
-        self.locs_in = torch.zeros(slots * self.loc_cap, dtype=loc_dtype, device=device)
-        self.counts_all = torch.zeros(world * slots * batch, dtype=count_dtype, device=device)
-        self.locs_all = torch.zeros(world * slots * self.loc_cap, dtype=loc_dtype, device=device)
+        self.sizes = np.asarray(sizes, dtype=np.int64)
+        self.needs = np.asarray(needs, dtype=np.int64)
+        if self.sizes.shape != self.needs.shape or self.sizes.ndim != 2:
+            raise ValueError("JobGather: sizes and needs must both be [world, nb]")
+        self.world, self.nb = self.sizes.shape
+        self.group, self.rank, self.pg = int(group), int(rank), pg
+        self.ngroups = -(-self.nb // self.group)
+        self.elt = torch.empty(0, dtype=dtype).element_size()
+        self.cnt = np.zeros((self.world, self.ngroups), np.int64)  # counts of rank r in group g
+        self.loc = np.zeros((self.world, self.ngroups), np.int64)  # locations of rank r in group g
+        for g in range(self.ngroups):
+            sl = slice(g * self.group, min(self.nb, (g + 1) * self.group))
+            self.cnt[:, g] = self.sizes[:, sl].sum(axis=1)
+            self.loc[:, g] = self.needs[:, sl].sum(axis=1)
+        self.slab = [max(1, int((self.cnt[:, g] + self.loc[:, g]).max())) for g in range(self.ngroups)]
+        self.inp = [torch.zeros(s, dtype=dtype, device=device) for s in self.slab]
+        # one rank: the slab is its own result (nothing to gather)
+        self.out = self.inp if self.world == 1 else [torch.zeros(self.world * s, dtype=dtype, device=device)
+                                                      for s in self.slab]
+
+    def _where(self, j: int):
+        g = j // self.group
+        return g, g * self.group
 
     def counts_slot(self, j: int):
-        return self.counts_in[j * self.batch:(j + 1) * self.batch]
+        g, j0 = self._where(j)
+        o = int(self.sizes[self.rank, j0:j].sum())
+        return self.inp[g][o:o + int(self.sizes[self.rank, j])]
 
     def locs_slot(self, j: int):
-        return self.locs_in[j * self.loc_cap:(j + 1) * self.loc_cap]
+        g, j0 = self._where(j)
+        o = int(self.cnt[self.rank, g] + self.needs[self.rank, j0:j].sum())
+        return self.inp[g][o:o + int(self.needs[self.rank, j])]
 
-    def gather(self, async_op: bool = False):
-        w1 = _all_gather_flat(self.counts_all, self.counts_in, self.group, async_op)
-        w2 = _all_gather_flat(self.locs_all, self.locs_in, self.group, async_op)
-        return (w1, w2) if async_op else None
+    def gather(self, g: int, async_op: bool = False):
+        """Group g's all-gather (enqueue it on a communication stream to
+        overlap it with the next launch); None with one rank."""
+        if self.world == 1:
+            return None
+        return _all_gather_flat(self.out[g], self.inp[g], self.pg, async_op)
 
-    def result(self, r: int, j: int, n: int):
-        """(offsets int64[n+1], locations[total]) of rank r's slot j."""
+    def gather_all(self):
+        for g in range(self.ngroups):
+            self.gather(g)
+
+    def assemble(self):
+        """The job's (offsets int64[total+1], locations) on the device, ranks
+        in order, then groups, then batches (= global pattern order for a
+        JobPlan)."""
         import torch
-        c0 = (r * self.slots + j) * self.batch
-        counts = self.counts_all[c0:c0 + n].to(torch.int64)
-        offsets = torch.zeros(n + 1, dtype=torch.int64, device=counts.device)
+        cnts, locs = [], []
+        for r in range(self.world):
+            for g in range(self.ngroups):
+                b = r * self.slab[g]
+                c, l = int(self.cnt[r, g]), int(self.loc[r, g])
+                cnts.append(self.out[g][b:b + c])
+                locs.append(self.out[g][b + c:b + c + l])
+        counts = torch.cat(cnts).to(torch.int64)
+        offsets = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=counts.device)
         torch.cumsum(counts, 0, out=offsets[1:])
-        l0 = (r * self.slots + j) * self.loc_cap
-        total = int(offsets[-1].item()) if n else 0
-        return offsets, self.locs_all[l0:l0 + total]
+        return offsets, torch.cat(locs)
 
-    def bytes_per_gather(self) -> int:
-        return (self.counts_all.numel() * self.counts_all.element_size()
-                + self.locs_all.numel() * self.locs_all.element_size())
+    def bytes_per_pass(self) -> int:
+        """Bytes every rank receives per pass over the job (all groups)."""
+        return sum(self.world * s for s in self.slab) * self.elt
+
+    def result_bytes(self) -> int:
+        """The job's own result bytes: every count and every location once."""
+        return int((self.cnt + self.loc).sum()) * self.elt
+
+
+def all_gather_ints(values: Sequence[int], device=None, pg=None) -> np.ndarray:
+    """Every rank's int vector (same length on every rank) -> int64[world, len]."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.int64, device=device)
+    if not (dist.is_available() and dist.is_initialized()):
+        return t.cpu().numpy()[None, :]
+    out = torch.zeros(dist.get_world_size(pg) * t.numel(), dtype=torch.int64, device=device)
+    _all_gather_flat(out, t, pg, False)
+    return out.view(-1, t.numel()).cpu().numpy()
 
 
 def concat(parts):

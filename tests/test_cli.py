@@ -130,6 +130,62 @@ def test_load_file_matches_load(pkg, O, tmp_path):
         f.close()
 
 
+def _direct_dir(tmp_path):
+    """A directory whose file system accepts O_DIRECT reads (tmpfs may not)."""
+    for d in (str(tmp_path), os.environ.get("GRAFT_REPO_ROOT", ""), ROOT, "/var/tmp"):
+        if not d or not os.path.isdir(d) or not os.access(d, os.W_OK):
+            continue
+        probe = os.path.join(d, ".fmx_odirect_probe")
+        try:
+            with open(probe, "wb") as f:
+                f.write(b"\0" * 8192)
+            fd = os.open(probe, os.O_RDONLY | os.O_DIRECT)
+            os.close(fd)
+            return d
+        except OSError:
+            continue
+        finally:
+            if os.path.exists(probe):
+                os.remove(probe)
+    return None
+
+
+@pytest.mark.gpu
+def test_load_file_direct(pkg, O, tmp_path):
+    """fmx_load_file with FMX_LOAD_DIRECT: the body read with O_DIRECT (page
+    cache bypassed, 4 KiB-rounded requests, the file's length not a multiple
+    of 4 KiB); chunk sizes that split the sections.  Results equal fmx_load's."""
+    d = _direct_dir(tmp_path)
+    if d is None:
+        pytest.skip("no writable file system here accepts O_DIRECT")
+    rng = np.random.default_rng(13)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=3_000_001).astype(np.uint8)
+    table = pkg.text_encoders.EncodingTable.from_symbols([b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"])
+    block = pkg.blocks.Block3(pkg.Vector.U64)
+    b = (pkg.FmIndexBuilder(text.size, 5, table, pkg.u32, block)
+         .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(3))
+         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(2)))
+    blob = pkg.aligned_buffer(b.blob_size())
+    b.build(text, blob)
+    assert blob.size % 4096 != 0
+    path = os.path.join(d, f"direct_{os.getpid()}.blob")
+    try:
+        blob.tofile(path)
+        pats = [text[s:s + int(rng.integers(6, 25))].tobytes() for s in rng.integers(0, text.size - 24, 5000)]
+        a = pkg.FmIndex.load(blob, pkg.u32, block, table)
+        want = a.locate_batch(pats)
+        a.close()
+        for chunk in (0, 1 << 20, (3 << 20) + 4096):
+            f = pkg.FmIndex.load_file(path, pkg.u32, block, pkg.text_encoders.EncodingTable, chunk_bytes=chunk,
+                                      direct=True)
+            got = f.locate_batch(pats)
+            assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), f"chunk {chunk}"
+            f.close()
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+
+
 @pytest.mark.gpu
 def test_load_file_threaded_ring(pkg, O, tmp_path):
     """A blob of ~80 MB: the default 16 MiB chunks are read by 4 threads

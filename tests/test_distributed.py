@@ -1,11 +1,16 @@
-"""World-size-2 tests of the multi-GPU plumbing on CPU (gloo): patterns are
-sharded across ranks, each rank answers its slab against its own replica of
-the index, and the concatenated result must equal the single-process answer.
-The per-rank compute here is the CPU oracle (this tests the sharding and the
-gather bench.py uses — sharding.ShardGather's fixed-size all-gathers and
-device-side assembly — not the kernels, which tests/test_gpu.py covers)."""
+"""Multi-rank plumbing on CPU (gloo): a job is dealt out by
+distributed.JobPlan, each rank answers its share against its own replica of
+the index, the results are gathered with one all-gather per launch group into
+exactly sized slabs (distributed.JobGather), and the job assembled from them
+must equal the single-process answer.  The per-rank compute here is the CPU
+oracle (this tests the sharding and the gather bench.py uses, not the kernels,
+which tests/test_gpu.py covers).  Also: bench.py's refusal to put several RCCL
+ranks on fewer GPUs."""
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -21,8 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, result_path):
-    import sys
+def _worker(rank, world, port, result_path, group, batch_target):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["FMX_NO_TORCH_RUNTIME"] = "1"
@@ -39,29 +43,33 @@ def _worker(rank, world, port, result_path):
     table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
     L = O.layout(4, 3, 64, 0)
     ix = O.OracleIndex(O.build(text, 5, L, 3, 2, table), L)
-    pats = [text[s:s + int(rng.integers(2, 14))] for s in rng.integers(0, len(text) - 14, size=1001)]
+    # 1001 patterns (ragged shards), 10-14 bytes: about one occurrence each
+    pats = [text[s:s + int(rng.integers(10, 15))] for s in rng.integers(0, len(text) - 14, size=1001)]
     data, offsets = pkg.pack_patterns(pats)
-    s, e = D.shard(len(pats), world, rank)
-    sd, so = D.slab_patterns(data, offsets, s, e)
-    loff, locs = ix.locate_batch(sd, so)
-    # the gather bench.py runs: fixed-size slots the results are written into,
-    # two all-gathers, no size exchange
-    cap = torch.tensor([locs.size], dtype=torch.int64)
-    dist.all_reduce(cap, op=dist.ReduceOp.MAX)  # a bound every rank's total stays under
-    sizes = D.shard_sizes(len(pats), world)
-    g = D.SlabGather(world, slots=2, batch=max(sizes), loc_cap=int(cap.item()), count_dtype=torch.int32,
-                     loc_dtype=torch.int32, device="cpu")
-    g.counts_slot(1)[:e - s] = torch.from_numpy(np.diff(loff).astype(np.int32))
-    g.locs_slot(1)[:locs.size] = torch.from_numpy(locs.astype(np.int32))
-    g.gather()
-    goff, glocs = D.concat([g.result(r, 1, sizes[r]) for r in range(world)])
+    plan = D.JobPlan(len(pats), world, batch_target, group)
+    # this rank's batches, answered; their location totals exchanged once
+    res = []
+    for a, b in plan.batches(rank):
+        sd, so = D.slab_patterns(data, offsets, a, b)
+        res.append(ix.locate_batch(sd, so) if b > a else (np.zeros(1, np.uint64), np.zeros(0, np.uint32)))
+    needs = D.all_gather_ints([int(o[-1]) for o, _ in res])
+    jg = D.JobGather(plan.sizes(), needs, group, rank, torch.int32, "cpu")
+    for j, (o, l) in enumerate(res):
+        jg.counts_slot(j).copy_(torch.from_numpy(np.diff(o).astype(np.int32)))
+        jg.locs_slot(j).copy_(torch.from_numpy(l.astype(np.int32)))
+    for gi in range(jg.ngroups):  # one collective per launch group
+        wk = jg.gather(gi, async_op=gi % 2 == 1)
+        if wk is not None:
+            wk.wait()
+    goff, glocs = jg.assemble()
     t = D.max_over_ranks(float(rank + 1))
     if rank == 0:
         ref_off, ref_locs = ix.locate_batch(data, offsets)
         ok = (np.array_equal(goff.numpy().astype(np.uint64), ref_off)
               and np.array_equal(glocs.numpy().astype(np.uint32), ref_locs) and t == float(world))
+        ratio = jg.bytes_per_pass() / jg.result_bytes()
         with open(result_path, "w") as f:
-            f.write("ok" if ok else "mismatch")
+            json.dump({"ok": bool(ok), "ratio": ratio, "groups": jg.ngroups}, f)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -75,10 +83,78 @@ def test_shard_partition(pkg):
             assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_matches_single(tmp_path, world):
-    """world 2 and 3 (ragged shards: 1001 patterns)."""
+@pytest.mark.parametrize("cfg,total", [("c3", 10_000_000), ("c5", 1_000_000)])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_job_plan_balanced(pkg, cfg, total, world):
+    """Every rank gets total/N patterns (within one), in the same number of
+    launch groups of GR = 8 batches; the batches tile each rank's slab."""
+    plan = pkg.distributed.JobPlan(total, world, 100_000, 8)
+    per_rank = [e - s for s, e in plan.spans]
+    assert max(per_rank) - min(per_rank) <= 1
+    assert all(abs(p - total / world) <= 1 for p in per_rank)
+    assert plan.nb % 8 == 0 and plan.groups == plan.nb // 8
+    sizes = plan.sizes()
+    assert sizes.shape == (world, plan.nb) and int(sizes.sum()) == total
+    assert sizes.max() - sizes.min() <= 1 and sizes.max() <= 100_000
+    for r in range(world):
+        b = plan.batches(r)
+        assert b[0][0] == plan.spans[r][0] and b[-1][1] == plan.spans[r][1]
+        assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    # the old deal: 10 x 100 k batches of C5 over 8 ranks gave ranks 0-1 twice the work
+    if cfg == "c5" and world == 8:
+        assert plan.nb == 8 and sizes.max() == 15_625
+
+
+def test_job_gather_slots_one_rank(pkg):
+    """World 1: the slab is the result; slots are exact, assembly is the
+    concatenation of every batch in order."""
+    import torch
+    D = pkg.distributed
+    plan = D.JobPlan(10, 1, 3, 2)
+    needs = [[1, 2, 3, 0]]
+    assert plan.sizes().tolist() == [[3, 3, 2, 2]]
+    jg = D.JobGather(plan.sizes(), needs, 2, 0, torch.int32, "cpu")
+    counts = [[1, 0, 0], [0, 1, 1], [1, 2], [0, 0]]
+    locs = [[7], [5, 9], [1, 2, 3], []]
+    for j in range(4):
+        assert jg.counts_slot(j).numel() == len(counts[j]) and jg.locs_slot(j).numel() == needs[0][j]
+        jg.counts_slot(j).copy_(torch.tensor(counts[j], dtype=torch.int32))
+        jg.locs_slot(j).copy_(torch.tensor(locs[j], dtype=torch.int32))
+    assert jg.gather(0) is None
+    off, loc = jg.assemble()
+    flat = [c for cs in counts for c in cs]
+    assert off.tolist() == [0] + list(np.cumsum(flat))
+    assert loc.tolist() == [7, 5, 9, 1, 2, 3] and int(off[-1]) == loc.numel()
+    assert jg.bytes_per_pass() == jg.result_bytes()
+
+
+@pytest.mark.parametrize("world,group,target", [(2, 2, 100), (3, 4, 60)])
+def test_gloo_job_gather_matches_single(tmp_path, world, group, target):
+    """world 2 and 3 (ragged shards: 1001 patterns), several launch groups."""
     import torch.multiprocessing as mp
-    out = tmp_path / "res.txt"
-    mp.spawn(_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
-    assert out.read_text() == "ok"
+    out = tmp_path / "res.json"
+    mp.spawn(_worker, args=(world, _free_port(), str(out), group, target), nprocs=world, join=True)
+    r = json.loads(out.read_text())
+    assert r["ok"] and r["groups"] >= 2
+    assert r["ratio"] <= 1.25, r  # slabs padded only to the largest rank's share
+
+
+def test_bench_refuses_oversubscribed_rccl():
+    """`bench.py --gpus N` with more RCCL ranks than visible GPUs exits 2
+    before touching a GPU (here: no GPU at all; on a 1-GPU box: N = 2)."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("FMX_BENCH_BACKEND", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(max(n, 2))],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 2, p.stderr
+    assert "refusing to oversubscribe" in p.stderr
+
+
+def test_bench_gpus_must_match_world():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr

@@ -689,6 +689,128 @@ def test_status_is_per_stream(pkg, O):
     ix.close()
 
 
+def _hip_runtime():
+    """The HIP runtime this process already uses (torch's), for raw streams:
+    torch.cuda.Stream() hands out a pool of 32, but this test needs distinct
+    handles."""
+    import ctypes
+
+    import torch
+    torch.cuda.init()
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln)
+    hip = ctypes.CDLL(path)
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+def test_status_slots_recycled(pkg, O):
+    """An index holds 1024 status words; streams beyond that recycle the least
+    recently used word whose stream is idle: 2,300 distinct
+    streams, all alive, each run a count batch; every result is right and
+    every sync is clean.  A stream that latched an error and never synced
+    loses its word (and the bits) once recycled, and its new owner starts
+    clean; fmx_stream_release reports what a stream latched and frees its word."""
+    import ctypes
+
+    import torch
+    hip = _hip_runtime()
+    rng = np.random.default_rng(31)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=30_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    dev = torch.device("cuda:0")
+    pats = [text[s:s + 10].tobytes() for s in rng.integers(0, text.size - 10, size=500)]
+    want = ix.count_batch(pats)
+    data, offsets = pkg.pack_patterns(pats)
+    d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev)
+    o = torch.from_numpy(offsets.view(np.int64).copy()).to(dev)
+    bdata, boffsets = pkg.pack_patterns(pats[:5] + [b""] + pats[5:10])
+    bd = torch.from_numpy(np.concatenate([bdata, np.zeros(16, np.uint8)])).to(dev)
+    bo = torch.from_numpy(boffsets.view(np.int64).copy()).to(dev)
+    bc = torch.zeros(11, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def new_stream():
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        return s.value
+
+    streams, outs = [], []
+    try:
+        # a stream latches an error and is never synced
+        lost = new_stream()
+        streams.append(lost)
+        ix.count_batch_async(bd.data_ptr(), bo.data_ptr(), 11, bc.data_ptr(), stream=lost)
+        torch.cuda.synchronize()
+        for i in range(2300):
+            s = new_stream()
+            streams.append(s)
+            c = torch.zeros(len(pats), dtype=torch.int32, device=dev)
+            ix.count_batch_async(d.data_ptr(), o.data_ptr(), len(pats), c.data_ptr(), stream=s)
+            outs.append(c)
+            if i % 97 == 0:
+                ix.sync(s)
+        torch.cuda.synchronize()
+        for s in streams[-300:]:
+            ix.sync(s)  # clean: a recycled word was zeroed for its new owner
+        for c in outs[::50]:
+            assert np.array_equal(c.cpu().numpy().view(np.uint32), want)
+        ix.sync(lost)  # its word went to another stream: nothing left to report
+        # fmx_stream_release: reports the latched error once, frees the word
+        r = new_stream()
+        streams.append(r)
+        ix.count_batch_async(bd.data_ptr(), bo.data_ptr(), 11, bc.data_ptr(), stream=r)
+        with pytest.raises(pkg.FmxError) as e:
+            ix.release_stream(r)
+        assert e.value.code == pkg._native.FMX_E_EMPTY_PATTERN
+        ix.sync(r)
+        c = torch.zeros(len(pats), dtype=torch.int32, device=dev)
+        ix.count_batch_async(d.data_ptr(), o.data_ptr(), len(pats), c.data_ptr(), stream=r)
+        ix.release_stream(r)
+        assert np.array_equal(c.cpu().numpy().view(np.uint32), want)
+        ix.sync()
+    finally:
+        torch.cuda.synchronize()
+        for s in streams:
+            hip.hipStreamDestroy(s)
+        ix.close()
+
+
+def test_locate_split_timers(pkg, O):
+    """Timing a grouped locate yields the launch and its two kernels
+    (locate.search, locate.emit): same launch count, search + emit = launch."""
+    import torch
+    rng = np.random.default_rng(5)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_000).astype(np.uint8)
+    blob = gpu_build(pkg, text.tobytes(), 5, 4, 3, 64, 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
+    dev = torch.device("cuda:0")
+    n, m = 20_000, 16
+    starts = rng.integers(0, text.size - m, size=n)
+    data = torch.from_numpy(np.stack([text[s:s + m] for s in starts]).reshape(-1).copy()).to(dev)
+    off = torch.arange(n + 1, dtype=torch.int64, device=dev) * m
+    loff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    locs = torch.zeros(4 * n, dtype=torch.int32, device=dev)
+    need = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = torch.zeros(ix.locate_workspace_size(n), dtype=torch.uint8, device=dev)
+    q = ix.job_queue([ix.locate_job(data.data_ptr(), off.data_ptr(), n, loff.data_ptr(), locs.data_ptr(), 4 * n,
+                                    need.data_ptr(), ws.data_ptr(), ws.numel(), fixed_len=m)])
+    ix.timing_enable(True)
+    for _ in range(6):
+        ix.locate_group_async(q)
+    t = ix.timing_read()
+    ix.timing_enable(False)
+    assert t["locate"]["launches"] == t["locate.search"]["launches"] == t["locate.emit"]["launches"] == 6
+    total = t["locate"]["total_ms"]
+    assert abs(t["locate.search"]["total_ms"] + t["locate.emit"]["total_ms"] - total) <= 0.02 * total + 1e-3
+    assert t["locate.search"]["units"] == 6 * n
+    ix.sync()
+    ix.close()
+
+
 def test_concurrent_host_threads(pkg, O):
     """One index driven from several host threads at once (fmx.h: an index is
     thread-safe): 4 threads each run the host-buffer API (count + locate,

@@ -1,0 +1,88 @@
+"""bench.py on the GPU, run as the driver runs it (a child process): the C3 job
+at full size through the strong-scaling path (JobPlan + JobGather) with every
+count and location checked against the oracle; several ranks rehearsed on one
+GPU over gloo; RCCL oversubscription refused."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(args, env_extra=None, timeout=900):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FMX_BENCH_BACKEND", "FMX_BENCH_DIST"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, capture_output=True,
+                       text=True, timeout=timeout, env=env)
+    sys.stderr.write(p.stderr[-4000:])
+    return p
+
+
+def last_json(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out
+    return json.loads(lines[-1])
+
+
+def test_c3_full_job_one_gpu():
+    """BASELINE configs[2] (10 M x 20 bp over 1 Gbp) on one GPU: the job is
+    planned (104 batches of ~96 k, 13 launch groups of 8), every launch's
+    results are written into the exactly sized gather slabs, the job's flat
+    (offsets, locations) is assembled on the device, and rank 0 compares all
+    10 M counts and every location with the CPU oracle."""
+    p = run_bench(["--config", "c3", "--verify-job", "--no-cpu", "--no-blob-layout", "--min-seconds", "0.05",
+                   "--warmup", "0"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = last_json(p.stdout)
+    assert r["scaling"] == "strong" and r["config"]["global_batch"] == 10_000_000
+    assert r["parity"]["scope"] == "every pattern of the job" and r["parity"]["patterns"] == 10_000_000
+    assert r["parity"]["bit_exact_vs_cpu"], r["parity"]
+    g = r["gather"]
+    assert g["assembly_ok"] and g["needs_stable"] and g["assembled_patterns"] == 10_000_000
+    assert g["plan"]["batches_per_rank"] % 8 == 0
+    assert r["self_location_check"] and r["n_gpus"] == 1 and r["ranks"] == 1
+
+
+def test_rccl_oversubscription_refused():
+    """Two RCCL ranks on a one-GPU box: refused before any GPU work."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    p = run_bench(["--gpus", str(n)], timeout=300)
+    assert p.returncode == 2 and "refusing to oversubscribe" in p.stderr
+
+
+def test_gloo_two_ranks_one_gpu_strong():
+    """FMX_BENCH_BACKEND=gloo bench.py --gpus 2: bench.py starts both ranks
+    itself; they share cuda:0 and the line says so (n_gpus 1, ranks 2, no RCCL
+    world).  A sharded job with the in-step gathers (one collective per launch
+    group); the assembled job equals the oracle's answer."""
+    p = run_bench(["--gpus", "2", "--config", "c3", "--text-len", "50000000", "--total-patterns", "800000",
+                   "--verify-job", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
+                  env_extra={"FMX_BENCH_BACKEND": "gloo"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = last_json(p.stdout)
+    assert r["n_gpus"] == 1 and r["ranks"] == 2 and r["rccl_world_size"] is None and r["backend"] == "gloo"
+    g = r["gather"]
+    assert g["inside_timed_step"] and g["collectives_per_launch"] == 1 and g["assembly_ok"]
+    assert g["gathered_over_result"] <= 1.25
+    assert g["plan"]["patterns_per_rank"] == [400_000, 400_000]
+    assert r["parity"]["bit_exact_vs_cpu"] and r["parity"]["patterns"] == 800_000
+
+
+def test_gloo_two_ranks_weak_gather():
+    """c2-style weak scaling on two ranks (gloo, one GPU): after the timed
+    region every batch is gathered in one exactly sized collective and this
+    rank's part comes back intact."""
+    p = run_bench(["--gpus", "2", "--config", "c2", "--text-len", "20000000", "--patterns", "20000",
+                   "--steps", "16", "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
+                  env_extra={"FMX_BENCH_BACKEND": "gloo"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = last_json(p.stdout)
+    assert r["ranks"] == 2 and r["n_gpus"] == 1 and r["scaling"] == "weak"
+    assert r["gather"]["roundtrip_ok"] and r["gather"]["bytes_gathered"] <= 1.25 * r["gather"]["result_bytes"]
