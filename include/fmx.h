@@ -279,7 +279,8 @@ fmx_status fmx_stream_release(fmx_index *ix, void *stream);
 /* --------------------------------------------------------------- timing
  * enable = k > 0: every k-th kernel launch (k = 1: every launch) is bracketed
  * by hipEvents on its stream; 0: off.  fmx_timing_read sums the bracketed
- * durations per kernel (it synchronises).  An event pair costs the stream
+ * durations per kernel since timing was last enabled (enabling resets the
+ * totals; fmx_timing_read synchronises).  An event pair costs the stream
  * several microseconds, so throughput runs sample (k > 1).  Timers: "count",
  * "locate" (a whole locate launch) and, for fmx_locate_group_async, its two
  * kernels "locate.search" (k_search) and "locate.emit" (k_emit). */

@@ -47,7 +47,8 @@ def main():
     b = bench_json(os.path.join(g, f"{tag}_fetch.log"))
     key = b["profile_key"]
     variant = ", 0>" if b["config"]["load_options"] in (0, 1) else ""
-    ppl = b["roofline"]["patterns_per_launch"]
+    rf = b["roofline"]
+    ppl = rf["kernel"]["patterns_per_launch"] if "kernel" in rf else rf["patterns_per_launch"]
     fetch, nl = sums(os.path.join(g, f"{tag}_fetch", "run_counter_collection.csv"), variant)
     ea, nl2 = sums(os.path.join(g, f"{tag}_ea", "run_counter_collection.csv"), variant)
     wr, nl3 = sums(os.path.join(g, f"{tag}_write", "run_counter_collection.csv"), variant)

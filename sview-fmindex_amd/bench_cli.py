@@ -174,6 +174,44 @@ def read_file(pkg, path: str, threads: int = 8) -> np.ndarray:
     return blob
 
 
+def resident_fraction(path: str) -> float:
+    """Share of the file's pages in the page cache (mincore over a read-only
+    mapping, which itself reads nothing); -1 if it cannot be determined."""
+    import ctypes
+    import mmap
+    size = os.path.getsize(path)
+    if size == 0:
+        return 0.0
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.mincore.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        with open(path, "rb") as f:
+            mm = mmap.mmap(f.fileno(), size, prot=mmap.PROT_READ)
+        try:
+            view = np.frombuffer(mm, np.uint8)
+            vec = np.zeros((size + mmap.PAGESIZE - 1) // mmap.PAGESIZE, np.uint8)
+            rc = libc.mincore(ctypes.c_void_p(view.ctypes.data), size, ctypes.c_void_p(vec.ctypes.data))
+            del view
+            return float((vec & 1).mean()) if rc == 0 else -1.0
+        finally:
+            mm.close()
+    except (OSError, ValueError, AttributeError, BufferError):
+        return -1.0
+
+
+def drop_file_cache(path: str) -> None:
+    """Evict the file's pages from the page cache without root: flush dirty
+    pages (a freshly built blob is dirty), then POSIX_FADV_DONTNEED — for this
+    file what the reference bench's `sync; echo 3 > /proc/sys/vm/drop_caches`
+    does machine-wide (bench/run_benchmark.sh:53-56)."""
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+    finally:
+        os.close(fd)
+
+
 def format_results(loc_offsets: np.ndarray, locs: np.ndarray) -> bytes:
     """One line per pattern, locations comma-joined (write_locations_to_file,
     locate/mod.rs:115-124).  Vectorised: every location becomes its digits
@@ -196,13 +234,15 @@ def format_results(loc_offsets: np.ndarray, locs: np.ndarray) -> bytes:
 
 
 def locate(data_dir: str, algorithm: str, treat_t_as_wildcard: bool, drop_caches: bool = False,
-           batch: int = 1 << 20, device: int = 0, options=None):
+           batch: int = 1 << 20, device: int = 0, options=None, direct: bool = False):
+    """`drop_caches`: the blob and pattern files are evicted from the page
+    cache before each load (drop_file_cache), so "Blob loading time" is a
+    cold read from storage, as in the reference's README runs; `direct`: the
+    sview-mmap loader reads the blob with O_DIRECT (FMX_LOAD_DIRECT)."""
     pkg = _pkg()
     pattern_path = os.path.join(data_dir, "pattern.txt")
     if not os.path.exists(pattern_path):
         raise SystemExit(f"Pattern file not found: {pattern_path}")
-    if drop_caches:
-        print("--drop-caches: not done here (needs root); blob reads may hit the page cache")
     _, block, tag = _layout(pkg, treat_t_as_wildcard)
     algos = ALGORITHMS if algorithm == "all" else (algorithm,)
     results = []
@@ -214,10 +254,15 @@ def locate(data_dir: str, algorithm: str, treat_t_as_wildcard: bool, drop_caches
                 continue
             raise SystemExit(f"{tag} blob file not found: {blob_path}")
         print(f"Using blob file: {blob_path}")
+        if drop_caches:
+            for f in (blob_path, pattern_path):
+                drop_file_cache(f)
+            print(f"Page cache dropped for the blob and pattern files: {resident_fraction(blob_path):.4f} of the "
+                  f"blob resident")
         t0 = time.perf_counter_ns()
         if a == "sview-mmap":
             ix = pkg.FmIndex.load_file(blob_path, pkg.u32, block, pkg.text_encoders.EncodingTable, device=device,
-                                       options=options)
+                                       options=options, direct=direct)
         else:
             blob = read_file(pkg, blob_path)
             if os.environ.get("FMX_LOAD_TRACE"):
@@ -281,7 +326,9 @@ def main(argv=None):
     lo.add_argument("-d", "--data-dir", default="test_data")
     lo.add_argument("-a", "--algorithm", default="all", choices=ALGORITHMS + ("all",))
     lo.add_argument("-t", "--treat-t-as-wildcard", action="store_true")
-    lo.add_argument("--drop-caches", action="store_true")
+    lo.add_argument("--drop-caches", action="store_true",
+                    help="evict the blob and pattern files from the page cache before each load (no root needed)")
+    lo.add_argument("--direct", action="store_true", help="sview-mmap: read the blob with O_DIRECT")
     lo.add_argument("--batch", type=int, default=1 << 20, help="patterns per fmx_locate_batch call")
     lo.add_argument("--device", type=int, default=0)
     lo.add_argument("--options", type=int, default=None,
@@ -298,7 +345,8 @@ def main(argv=None):
     elif a.command == "build":
         build(a.data_dir, a.algorithm, a.sasr, a.klts, a.treat_t_as_wildcard, a.device)
     elif a.command == "locate":
-        locate(a.data_dir, a.algorithm, a.treat_t_as_wildcard, a.drop_caches, a.batch, a.device, a.options)
+        locate(a.data_dir, a.algorithm, a.treat_t_as_wildcard, a.drop_caches, a.batch, a.device, a.options,
+               a.direct)
     print(f"Total time: {time.perf_counter_ns() - t0} ns")
     # the reference's run_benchmark.sh reads max RSS from /usr/bin/time -v
     import resource

@@ -322,6 +322,11 @@ static uint32_t *status_slot(fmx_index *ix, hipStream_t s, int *idx) {
 static void status_launched(fmx_index *ix, int idx, hipStream_t s) {
     std::lock_guard<std::mutex> g(ix->status_mu);
     StatusSlot &sl = ix->slots[idx];
+    if (!ix->status_events) {
+        sl.pinned = true;
+        if (sl.inflight) --sl.inflight;
+        return;
+    }
     if (!sl.done && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) sl.done = nullptr;
     if (sl.done && hipEventRecord(sl.done, s) == hipSuccess) sl.launched = true;
     else if (!sl.done) sl.pinned = true;  // (cannot tell when it completes: never recycle it)
@@ -375,6 +380,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     if (hipMemset(ix->d_status, 0, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     ix->slots.assign(kStatusSlots, StatusSlot{});
+    if (const char *ev = getenv("FMX_STATUS_EVENTS")) ix->status_events = ev[0] != '0';
     for (uint32_t i = kStatusSlots; i-- > 0;) ix->free_slots.push_back(i);
     {
         int idx = -1;
@@ -1071,6 +1077,19 @@ fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
     if (!ix) return FMX_E_ARG;
     if (enable < 0) return FMX_E_ARG;
     std::lock_guard<std::mutex> g(ix->timing_mu);
+    if (enable) {  // a fresh measurement: totals (and spans not read yet) start from zero
+        for (auto &t : ix->timers) {
+            for (const TimedSpan &p : t.pending) {
+                if (hipEventSynchronize(p.b) != hipSuccess) return FMX_E_DEVICE;
+                if (p.own_a) ix->event_pool.push_back(p.a);
+                if (p.own_b) ix->event_pool.push_back(p.b);
+            }
+            t.pending.clear();
+            t.launches = 0;
+            t.ms = 0.0;
+            t.units = 0;
+        }
+    }
     ix->timing = enable != 0;
     ix->timing_every = enable > 0 ? (uint32_t)enable : 1u;
     ix->timing_seq = 0;

@@ -15,7 +15,8 @@
 // Sizes: n + 1 < 2^32 with 32-bit suffix indices (about 40 B per text byte of
 // transient HBM at the peak: keys, values and their double buffers); larger
 // texts take the bucketed 64-bit path (suffix_array64: ~17 B per text byte
-// plus ~40 B per element of the largest first-two-symbol bucket).
+// plus ~49 B per element of the largest first-two-symbol bucket and 56 B per
+// suffix still unresolved in a doubling round).
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -425,7 +426,9 @@ static fmx_status suffix_array(const uint8_t *t, uint64_t n1, uint32_t alphabet,
 // group-head rank.  The doubling rounds sort only the unresolved groups: by
 // rank(i + h), then stably by rank(i) (both 64-bit keys, two stable radix
 // sorts: a 128-bit key in two passes).  Transient HBM: t + sa + isa (17 B per
-// text byte) plus ~40 B per element of the largest bucket / active set.
+// text byte) plus ~49 B per element of the largest bucket (first sort) and
+// 56 B per unresolved slot in a doubling round (six 8-B buffers reused across
+// the round's steps + the slot list).
 
 __global__ __launch_bounds__(256) void k_bucket_of(const uint8_t *__restrict__ t, uint64_t n1, uint32_t W,
                                                    uint32_t *__restrict__ hist) {
@@ -665,41 +668,42 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
     uint64_t *A = alist.as<uint64_t>();
     for (uint64_t h = K0; m > 0; h *= 2) {
         if (h >= n1) return FMX_E_CONFIG;  // impossible with a unique sentinel
-        DBuf kA, kB, vA, vB, pri, idx, idx2, sec2, val2, hv, hj, fl, A2;
+        // six buffers of m words, reused across the round's steps (48 B per
+        // active slot, + 8 B of the slot list): after each double-buffered
+        // sort the alternate buffers are free and take the next step's output
+        DBuf kA, kB, vA, vB, xA, xB;
         BCK(kA.alloc(m * 8)); BCK(kB.alloc(m * 8)); BCK(vA.alloc(m * 8)); BCK(vB.alloc(m * 8));
+        BCK(xA.alloc(m * 8)); BCK(xB.alloc(m * 8));
         uint64_t *k1 = kA.as<uint64_t>(), *k2 = kB.as<uint64_t>(), *v1 = vA.as<uint64_t>(), *v2 = vB.as<uint64_t>();
         hipLaunchKernelGGL(k_round_sec, dim3(grid_of(m)), dim3(256), 0, s, A, m, sa, ISA, h, k1, v1);
         BCK(hipGetLastError());
-        BCK(sort_pairs_db(k1, k2, v1, v2, m, 0, 64, s));  // by rank(i + h)
-        BCK(pri.alloc(m * 8)); BCK(idx.alloc(m * 8)); BCK(idx2.alloc(m * 8)); BCK(sec2.alloc(m * 8));
-        BCK(val2.alloc(m * 8));
-        uint64_t *p1 = pri.as<uint64_t>(), *p2 = k2, *i1 = idx.as<uint64_t>(), *i2 = idx2.as<uint64_t>();
+        BCK(sort_pairs_db(k1, k2, v1, v2, m, 0, 64, s));  // by rank(i + h); k2, v2 now free
+        uint64_t *p1 = xA.as<uint64_t>(), *p2 = k2, *i1 = xB.as<uint64_t>(), *i2 = v2;
         hipLaunchKernelGGL(k_round_pri, dim3(grid_of(m)), dim3(256), 0, s, v1, m, ISA, p1, i1);
         BCK(hipGetLastError());
         BCK(sort_pairs_db(p1, p2, i1, i2, m, 0, 64, s));  // stably by rank(i): groups stay in slot order
-        hipLaunchKernelGGL(k_gather2, dim3(grid_of(m)), dim3(256), 0, s, i1, m, v1, k1, val2.as<uint64_t>(),
-                           sec2.as<uint64_t>());
+        uint64_t *val2 = i2, *sec2 = p2;                    // (the second sort's free buffers)
+        hipLaunchKernelGGL(k_gather2, dim3(grid_of(m)), dim3(256), 0, s, i1, m, v1, k1, val2, sec2);
         BCK(hipGetLastError());
-        BCK(hv.alloc(m * 8)); BCK(hj.alloc(m * 8)); BCK(fl.alloc(m));
-        hipLaunchKernelGGL(k_heads64, dim3(grid_of(m)), dim3(256), 0, s, p1, sec2.as<uint64_t>(), m,
-                           hv.as<uint64_t>(), fl.as<uint8_t>());
-        BCK(max_scan64(hv.as<uint64_t>(), hj.as<uint64_t>(), m, s));
-        hipLaunchKernelGGL(k_round_write64, dim3(grid_of(m)), dim3(256), 0, s, A, m, val2.as<uint64_t>(),
-                           hj.as<uint64_t>(), sa, ISA);
+        uint64_t *hv = v1, *hj = k1;                        // (free once gathered)
+        uint8_t *fl = reinterpret_cast<uint8_t *>(i1);
+        hipLaunchKernelGGL(k_heads64, dim3(grid_of(m)), dim3(256), 0, s, p1, sec2, m, hv, fl);
+        BCK(max_scan64(hv, hj, m, s));
+        hipLaunchKernelGGL(k_round_write64, dim3(grid_of(m)), dim3(256), 0, s, A, m, val2, hj, sa, ISA);
         BCK(hipGetLastError());
-        // the next round's active slots: A[j] where fl[j]
-        BCK(A2.alloc(m * 8));
+        // the next round's active slots: A[j] where fl[j] (into hv: scanned already)
+        uint64_t *A2 = hv;
         uint64_t m2 = 0;
         {
             size_t tb = 0;
-            BCK(rocprim::select(nullptr, tb, A, fl.as<uint8_t>(), A2.as<uint64_t>(), cntd.as<uint64_t>(), m, s));
+            BCK(rocprim::select(nullptr, tb, A, fl, A2, cntd.as<uint64_t>(), m, s));
             BCK(with_temp(tb, [&](void *tmp) {
-                return rocprim::select(tmp, tb, A, fl.as<uint8_t>(), A2.as<uint64_t>(), cntd.as<uint64_t>(), m, s);
+                return rocprim::select(tmp, tb, A, fl, A2, cntd.as<uint64_t>(), m, s);
             }));
             BCK(hipMemcpyAsync(&m2, cntd.p, 8, hipMemcpyDeviceToHost, s));
             BCK(hipStreamSynchronize(s));
         }
-        BCK(hipMemcpyAsync(A, A2.p, m2 * 8, hipMemcpyDeviceToDevice, s));
+        BCK(hipMemcpyAsync(A, A2, m2 * 8, hipMemcpyDeviceToDevice, s));
         m = m2;
     }
     BCK(hipStreamSynchronize(s));

@@ -141,6 +141,7 @@ struct fmx_index {
     std::unordered_map<const void *, uint32_t> status_of;  // stream -> slot
     std::vector<uint32_t> free_slots;
     uint64_t status_clock = 0;
+    bool status_events = true;  // FMX_STATUS_EVENTS=0: no completion events (A/B; words never recycled)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
