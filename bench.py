@@ -116,6 +116,9 @@ def parse():
     ap.add_argument("--options", type=int, default=FAITHFUL,
                     help="fmx_load options of the headline index (1 = FMX_OCC_INTERLEAVED, 0 = blob layout)")
     ap.add_argument("--no-blob-layout", action="store_true", help="skip the blob-layout (options 0) leg")
+    ap.add_argument("--blob-source", choices=("broadcast", "build"), default="broadcast",
+                    help="several ranks: rank 0 builds the blob and broadcasts it over RCCL (SURVEY 8(e)), or "
+                         "every rank builds its own (deterministic)")
     ap.add_argument("--derived", action="store_true", help="also run the derived-index leg (~147 GB at C2)")
     ap.add_argument("--derived-options", type=int, default=DERIVED)
     ap.add_argument("--no-derived", action="store_true", help=argparse.SUPPRESS)  # (the default now)
@@ -484,10 +487,20 @@ def main():
     d_blob = torch.empty(blob_len, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     t1 = time.time()
-    builder.build_device(d_text.data_ptr(), d_blob.data_ptr(), blob_len, device=gpu)
+    bcast = dist_on and world > 1 and args.blob_source == "broadcast"
+    if rank == 0 or not bcast:
+        builder.build_device(d_text.data_ptr(), d_blob.data_ptr(), blob_len, device=gpu)
     torch.cuda.synchronize()
     build_s = time.time() - t1
     log(f"[rank {rank}] text {n:,} B generated in {t1 - t0:.2f}s, blob {blob_len:,} B built on GPU in {build_s:.2f}s")
+    replicate = None
+    if bcast:
+        # one replica per GPU: rank 0's blob broadcast over RCCL (xGMI), then
+        # every rank's copy checksummed and compared across ranks
+        replicate = D.replicate_blob(d_blob, src=0)
+        replicate["gbs"] = blob_len / replicate["seconds"] / 1e9
+        if not replicate["identical"]:
+            raise SystemExit(f"rank {rank}: the broadcast blob differs across ranks")
 
     # PCIe: what loading this blob from host memory costs (pinned -> HBM)
     upload_s = None
@@ -755,6 +768,8 @@ def main():
         # end from a host-resident blob: upload + load + locate
         "readme_workload_s": None if upload_s is None else upload_s + load_s + 100_000 / per_gpu,
         "gather": gather,
+        "blob_replication": replicate if replicate else
+        {"how": "each rank builds the blob from the same seeded text" if world > 1 else "one rank"},
         "profile_key": key,
     }
 

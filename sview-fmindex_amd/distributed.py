@@ -174,6 +174,39 @@ def all_gather_ints(values: Sequence[int], device=None, pg=None) -> np.ndarray:
     return out.view(-1, t.numel()).cpu().numpy()
 
 
+def replicate_blob(d_blob, src: int = 0, group=None) -> dict:
+    """Broadcast rank src's blob (a uint8 tensor of the same size on every
+    rank) to every rank — SURVEY §8(e)'s replicated blob, over RCCL/xGMI —
+    then compare a checksum of every rank's copy.  Returns the broadcast's
+    seconds (barrier to barrier) and whether all copies are identical."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    def sync():
+        if d_blob.is_cuda:
+            torch.cuda.synchronize()
+
+    dist.barrier(group=group)
+    sync()
+    t0 = time.perf_counter()
+    dist.broadcast(d_blob, src=src, group=group)
+    sync()
+    dist.barrier(group=group)
+    sec = time.perf_counter() - t0
+    n8 = d_blob.numel() // 8 * 8
+    words = d_blob[:n8].view(torch.int64)
+    # two position-weighted sums (wrapping int64): equal on every rank iff
+    # the copies agree (up to a checksum collision)
+    w = torch.arange(1, words.numel() + 1, dtype=torch.int64, device=d_blob.device)
+    ck = torch.stack([words.sum(), (words * w).sum(), d_blob[n8:].to(torch.int64).sum()])
+    lo, hi = ck.clone(), ck.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    return {"how": f"built on rank {src}, broadcast to every rank", "seconds": sec,
+            "bytes": int(d_blob.numel()), "identical": bool(torch.equal(lo, hi))}
+
+
 def concat(parts):
     """Concatenate per-rank (offsets, locations) results in rank order into
     the (offsets, locations) one device would have produced for the union."""

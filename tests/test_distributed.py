@@ -74,6 +74,37 @@ def _worker(rank, world, port, result_path, group, batch_target):
     dist.destroy_process_group()
 
 
+def _bcast_worker(rank, world, port, result_path):
+    sys.path.insert(0, ROOT)
+    os.environ["FMX_NO_TORCH_RUNTIME"] = "1"
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+    D = g.load_package().distributed
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    blob = torch.zeros(100_003, dtype=torch.uint8)
+    if rank == 0:
+        blob.copy_(torch.from_numpy(np.random.default_rng(3).integers(0, 256, blob.numel(), dtype=np.uint8)))
+    r = D.replicate_blob(blob, src=0)
+    want = np.random.default_rng(3).integers(0, 256, blob.numel(), dtype=np.uint8)
+    ok = r["identical"] and np.array_equal(blob.numpy(), want) and r["bytes"] == blob.numel()
+    flags = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        with open(result_path, "w") as f:
+            f.write("ok" if int(flags) == 1 else "mismatch")
+    dist.destroy_process_group()
+
+
+def test_replicate_blob_gloo(tmp_path):
+    """Rank 0's blob broadcast to every rank; the cross-rank
+    checksum agrees; the odd length exercises the non-word tail."""
+    import torch.multiprocessing as mp
+    out = tmp_path / "bcast.txt"
+    mp.spawn(_bcast_worker, args=(3, _free_port(), str(out)), nprocs=3, join=True)
+    assert out.read_text() == "ok"
+
+
 def test_shard_partition(pkg):
     for n in (0, 1, 7, 100, 1001):
         for w in (1, 2, 3, 8):

@@ -73,6 +73,8 @@ def test_gloo_two_ranks_one_gpu_strong():
     assert g["gathered_over_result"] <= 1.25
     assert g["plan"]["patterns_per_rank"] == [400_000, 400_000]
     assert r["parity"]["bit_exact_vs_cpu"] and r["parity"]["patterns"] == 800_000
+    rep = r["blob_replication"]  # rank 0's blob broadcast to rank 1, checksums equal
+    assert rep["identical"] and rep["bytes"] > 0
 
 
 def test_gloo_two_ranks_weak_gather():
