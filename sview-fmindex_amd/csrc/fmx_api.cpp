@@ -264,14 +264,29 @@ struct LoadTrace {
 // The status word of `s`: every stream an index launches on gets a device
 // word of its own, so fmx_sync(s) reads and clears only what that stream's
 // launches latched (stream-ordered), never another stream's.  A stream seen
-// for the first time takes a free slot, or else the least recently used slot
-// whose launches have all completed (its `done` event): the slot changes
-// owner and its word is zeroed on the new stream before that stream's first
-// launch, so bits an earlier owner latched and never read are dropped
-// (fmx_sync or fmx_stream_release collect them).  Only when every slot's
-// stream still has launches in flight is there no slot (FMX_E_DEVICE).
-// `launch`: the slot is held (not recycled) until status_launched() records
-// the launch's completion event.  Caller holds status_mu.
+// for the first time takes a free word, or else recycles the least recently
+// used word whose stream is known to be idle: the word changes owner and is
+// zeroed on the new stream before that stream's first launch, so bits an
+// earlier owner latched and never read are dropped (fmx_sync or
+// fmx_stream_release collect them).  Idle is known from a completion event
+// recorded after each launch — only once 3/4 of the words are assigned
+// (pressure mode), since an event per launch costs ~1 % — or, for words
+// assigned before that, from one device-wide synchronisation when no word is
+// otherwise free (a process cycling through more than ~1,000 streams).
+// `launch`: the word is held until status_launched().  Caller holds status_mu.
+static int pick_recyclable(fmx_index *ix) {
+    int idx = -1;
+    uint64_t best = ~0ull;
+    for (uint32_t i = 0; i < ix->slots.size(); ++i) {
+        const StatusSlot &sl = ix->slots[i];
+        if (sl.pinned || sl.inflight || sl.maybe_busy || sl.last >= best) continue;
+        if (sl.launched && hipEventQuery(sl.done) != hipSuccess) continue;
+        best = sl.last;
+        idx = (int)i;
+    }
+    return idx;
+}
+
 static int status_slot_locked(fmx_index *ix, hipStream_t s, bool launch) {
     auto it = ix->status_of.find((const void *)s);
     if (it != ix->status_of.end()) {
@@ -286,13 +301,14 @@ static int status_slot_locked(fmx_index *ix, hipStream_t s, bool launch) {
         idx = (int)ix->free_slots.back();
         ix->free_slots.pop_back();
     } else {
-        uint64_t best = ~0ull;
-        for (uint32_t i = 0; i < ix->slots.size(); ++i) {
-            const StatusSlot &sl = ix->slots[i];
-            if (sl.pinned || sl.inflight || sl.last >= best) continue;
-            if (sl.launched && hipEventQuery(sl.done) != hipSuccess) continue;
-            best = sl.last;
-            idx = (int)i;
+        idx = pick_recyclable(ix);
+        if (idx < 0) {
+            // words assigned before pressure mode have no events: one device
+            // sync makes every word not held by a launch call idle
+            if (hipDeviceSynchronize() != hipSuccess) return -1;
+            for (auto &sl : ix->slots)
+                if (!sl.inflight) { sl.maybe_busy = false; sl.launched = false; }
+            idx = pick_recyclable(ix);
         }
         if (idx < 0) return -1;
         ix->status_of.erase(ix->slots[idx].key);
@@ -307,7 +323,9 @@ static int status_slot_locked(fmx_index *ix, hipStream_t s, bool launch) {
     sl.last = ++ix->status_clock;
     sl.inflight = 1;
     sl.launched = false;
+    sl.maybe_busy = false;
     ix->status_of.emplace((const void *)s, (uint32_t)idx);
+    if (ix->free_slots.size() < ix->slots.size() / 4) ix->status_pressure = true;
     return idx;
 }
 
@@ -317,20 +335,23 @@ static uint32_t *status_slot(fmx_index *ix, hipStream_t s, int *idx) {
     return *idx < 0 ? nullptr : ix->d_status + *idx;
 }
 
-// After the launch(es) of a status_slot() call were queued on s: record the
-// slot's completion event and release the hold.
+// After the launch(es) of a status_slot() call were queued on s: release the
+// hold and note how the word's idleness will be known (pressure mode: an event).
 static void status_launched(fmx_index *ix, int idx, hipStream_t s) {
     std::lock_guard<std::mutex> g(ix->status_mu);
     StatusSlot &sl = ix->slots[idx];
-    if (!ix->status_events) {
-        sl.pinned = true;
-        if (sl.inflight) --sl.inflight;
-        return;
-    }
-    if (!sl.done && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) sl.done = nullptr;
-    if (sl.done && hipEventRecord(sl.done, s) == hipSuccess) sl.launched = true;
-    else if (!sl.done) sl.pinned = true;  // (cannot tell when it completes: never recycle it)
     if (sl.inflight) --sl.inflight;
+    if (sl.pinned) return;
+    if (ix->status_pressure) {
+        if (!sl.done && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) sl.done = nullptr;
+        if (sl.done && hipEventRecord(sl.done, s) == hipSuccess) {
+            sl.launched = true;
+            sl.maybe_busy = false;
+            return;
+        }
+    }
+    sl.launched = false;
+    sl.maybe_busy = true;
 }
 
 // status_slot + status_launched around one launch function.
@@ -380,7 +401,6 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     if (hipMemset(ix->d_status, 0, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     ix->slots.assign(kStatusSlots, StatusSlot{});
-    if (const char *ev = getenv("FMX_STATUS_EVENTS")) ix->status_events = ev[0] != '0';
     for (uint32_t i = kStatusSlots; i-- > 0;) ix->free_slots.push_back(i);
     {
         int idx = -1;
@@ -944,8 +964,10 @@ fmx_status fmx_stream_release(fmx_index *ix, void *stream) {
     std::lock_guard<std::mutex> g(ix->status_mu);
     auto it = ix->status_of.find((const void *)s);
     if (it != ix->status_of.end() && !ix->slots[it->second].pinned && ix->slots[it->second].inflight == 0) {
-        ix->slots[it->second].key = nullptr;
-        ix->slots[it->second].launched = false;
+        StatusSlot &sl = ix->slots[it->second];
+        sl.key = nullptr;
+        sl.launched = false;
+        sl.maybe_busy = false;
         ix->free_slots.push_back(it->second);
         ix->status_of.erase(it);
     }

@@ -110,16 +110,19 @@ struct Timer {
     std::vector<TimedSpan> pending;
 };
 
-// A status word's owner: the stream it is assigned to, the event recorded
-// after that stream's latest launch (a slot is recycled only once it has
-// completed), and its recency for least-recently-used recycling.
+// A status word's owner: the stream it is assigned to, its recency (for
+// least-recently-used recycling) and what is known about its launches: a
+// slot is recycled only when its stream is known to be idle.  Completion
+// events are recorded only once the words run short (pressure mode): one per
+// launch costs ~1 % of throughput (profiles/r3/r3b_status_events.txt).
 struct StatusSlot {
     const void *key = nullptr;
     hipEvent_t done = nullptr;
     uint64_t last = 0;
-    uint32_t inflight = 0;  // assigned to a launch that has not recorded `done` yet
-    bool launched = false;
-    bool pinned = false;    // the index's own stream: never recycled
+    uint32_t inflight = 0;   // held by a launch call in progress
+    bool launched = false;   // `done` follows the stream's latest launch
+    bool maybe_busy = false; // launched without an event: idle only after a device sync
+    bool pinned = false;     // the index's own stream: never recycled
 };
 
 }  // namespace fmx
@@ -141,7 +144,7 @@ struct fmx_index {
     std::unordered_map<const void *, uint32_t> status_of;  // stream -> slot
     std::vector<uint32_t> free_slots;
     uint64_t status_clock = 0;
-    bool status_events = true;  // FMX_STATUS_EVENTS=0: no completion events (A/B; words never recycled)
+    bool status_pressure = false;  // most words assigned: launches record completion events
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
