@@ -255,10 +255,12 @@ def locate(data_dir: str, algorithm: str, treat_t_as_wildcard: bool, drop_caches
             raise SystemExit(f"{tag} blob file not found: {blob_path}")
         print(f"Using blob file: {blob_path}")
         if drop_caches:
+            td = time.perf_counter_ns()
             for f in (blob_path, pattern_path):
                 drop_file_cache(f)
-            print(f"Page cache dropped for the blob and pattern files: {resident_fraction(blob_path):.4f} of the "
-                  f"blob resident")
+            print(f"Page cache dropped for the blob and pattern files in {time.perf_counter_ns() - td} ns (outside "
+                  f"the timings below, as the reference's drop_caches): {resident_fraction(blob_path):.4f} of "
+                  f"the blob resident")
         t0 = time.perf_counter_ns()
         if a == "sview-mmap":
             ix = pkg.FmIndex.load_file(blob_path, pkg.u32, block, pkg.text_encoders.EncodingTable, device=device,

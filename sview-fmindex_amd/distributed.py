@@ -17,6 +17,10 @@ CPU for tests).  No collective runs inside the query path itself.
   the largest rank's share.  `assemble()` concatenates the gathered slabs on
   the device into the job's flat (offsets, locations) — the answer one
   device would give for the whole job — with no host round trip per slot.
+- `ShardedLocate` is the same for one global batch as a call: every rank
+  passes the batch, locates its shard, one packed all-gather, and every rank
+  gets the batch's (offsets, locations).
+- `replicate_blob` broadcasts rank 0's blob to every rank (RCCL over xGMI).
 """
 from __future__ import annotations
 
@@ -160,6 +164,90 @@ class JobGather:
     def result_bytes(self) -> int:
         """The job's own result bytes: every count and every location once."""
         return int((self.cnt + self.loc).sum()) * self.elt
+
+
+class ShardedLocate:
+    """`FmIndex.locate_batch` for one global batch over every rank of a
+    process group — the north star's "pattern batches shard across the GPUs,
+    blob replicated, one all-gather concatenates the results" as a call.
+
+    Every rank passes the same batch (device bytes + int64 offsets[n+1]);
+    rank r locates the contiguous shard `shard(n, world, r)` on its own GPU
+    against its own replica of the index, writing its counts and locations
+    into one packed slab [counts | locations]; after a 16-byte size exchange
+    one all_gather_into_tensor moves every rank's slab, and the batch's flat
+    (offsets int64[n+1], locations) is assembled on the device — identical on
+    every rank and equal to one device's answer for the whole batch.
+
+    `locate_fn(d_bytes, d_offsets, m, counts_out, locs_out, cap) -> needed`
+    runs the shard (FmIndex by default: fmx_locate_batch_async on `stream`);
+    if the shard has more occurrences than the first guess of room, it runs
+    again with exactly enough.  Host round trips per call: the shard's byte
+    range, its location total and the size exchange."""
+
+    def __init__(self, ix=None, dtype=None, device=None, group=None, locate_fn=None, stream=None):
+        import torch
+        import torch.distributed as dist
+        self.dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist_on else 1
+        self.rank = dist.get_rank(group) if self.dist_on else 0
+        self.group, self.device, self.stream = group, device, stream
+        self.ix = ix
+        self.dtype = dtype or (torch.int32 if ix is None or ix.position.nbytes == 4 else torch.int64)
+        self.locate_fn = locate_fn or self._index_locate
+        self._ws = None
+        self.last = {}
+
+    def _index_locate(self, d_bytes, d_offsets, m, counts, locs, cap):
+        import torch
+        ws = self.ix.locate_workspace_size(max(m, 1))
+        if self._ws is None or self._ws.numel() < ws:
+            self._ws = torch.zeros(ws, dtype=torch.uint8, device=d_offsets.device)
+        loff = torch.zeros(m + 1, dtype=torch.int64, device=d_offsets.device)
+        need = torch.zeros(1, dtype=torch.int64, device=d_offsets.device)
+        st = self.stream.cuda_stream if self.stream is not None else 0
+        self.ix.locate_batch_async(d_bytes.data_ptr() if d_bytes.numel() else 0, d_offsets.data_ptr(), m,
+                                   loff.data_ptr(), locs.data_ptr() if cap else 0, cap, need.data_ptr(),
+                                   self._ws.data_ptr(), self._ws.numel(), d_counts=counts.data_ptr() if m else 0,
+                                   stream=st)
+        self.ix.sync(st)
+        return int(need.item())
+
+    def locate(self, d_bytes, d_offsets):
+        import torch
+        n = int(d_offsets.numel()) - 1
+        s, e = shard(n, self.world, self.rank)
+        m = e - s
+        dev = d_offsets.device
+        b = d_offsets[[s, e]].cpu().tolist() if n >= 0 else [0, 0]
+        sub_off = (d_offsets[s:e + 1] - b[0]).contiguous()
+        sub_bytes = d_bytes[b[0]:b[1]]
+        cap = m + m // 8 + 4096
+        slab = torch.zeros(m + cap, dtype=self.dtype, device=dev)
+        need = self.locate_fn(sub_bytes, sub_off, m, slab[:m], slab[m:], cap)
+        if need > cap:  # more occurrences than guessed: run again with room for all of them
+            slab = torch.zeros(m + need, dtype=self.dtype, device=dev)
+            got = self.locate_fn(sub_bytes, sub_off, m, slab[:m], slab[m:], need)
+            if got != need:
+                raise RuntimeError(f"ShardedLocate: location total changed between runs ({need} -> {got})")
+        parts = all_gather_ints([m, need], device=dev, pg=self.group)  # [world, 2]
+        S = max(1, int((parts[:, 0] + parts[:, 1]).max()))
+        if slab.numel() < S:
+            slab = torch.cat([slab, torch.zeros(S - slab.numel(), dtype=self.dtype, device=dev)])
+        inp = slab[:S].contiguous()
+        if self.world == 1:
+            out = inp
+        else:
+            out = torch.zeros(self.world * S, dtype=self.dtype, device=dev)
+            _all_gather_flat(out, inp, self.group, False)
+        cnts = [out[r * S:r * S + int(parts[r, 0])] for r in range(self.world)]
+        locs = [out[r * S + int(parts[r, 0]):r * S + int(parts[r, 0] + parts[r, 1])] for r in range(self.world)]
+        counts = torch.cat(cnts).to(torch.int64)
+        offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(counts, 0, out=offsets[1:])
+        self.last = {"patterns": n, "shard": (s, e), "bytes_gathered": self.world * S * inp.element_size(),
+                     "result_bytes": int((parts[:, 0] + parts[:, 1]).sum()) * inp.element_size()}
+        return offsets, torch.cat(locs)
 
 
 def all_gather_ints(values: Sequence[int], device=None, pg=None) -> np.ndarray:

@@ -105,6 +105,61 @@ def test_replicate_blob_gloo(tmp_path):
     assert out.read_text() == "ok"
 
 
+def _sharded_worker(rank, world, port, result_path):
+    """ShardedLocate with the oracle as each rank's locate: one global batch
+    (ragged, with high-count short patterns that overflow the first guess of
+    room), every rank gets the whole batch's answer."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["FMX_NO_TORCH_RUNTIME"] = "1"
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+    from oracle import oracle as O
+    from _util import table_from_symbols
+    D = g.load_package().distributed
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    rng = np.random.default_rng(9)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=30000).astype(np.uint8).tobytes()
+    L = O.layout(4, 3, 64, 0)
+    ix = O.OracleIndex(O.build(text, 5, L, 3, 2, table_from_symbols([b"A", b"C", b"G", b"T", b"N"])), L)
+    pats = [text[s:s + int(rng.integers(1, 16))] for s in rng.integers(0, len(text) - 16, size=2001)]
+    data = np.frombuffer(b"".join(pats), np.uint8).copy()
+    offs = np.zeros(len(pats) + 1, np.int64)
+    offs[1:] = np.cumsum([len(p) for p in pats])
+
+    def oracle_locate(d_bytes, d_offsets, m, counts, locs, cap):
+        o, l = ix.locate_batch(d_bytes.numpy(), d_offsets.numpy().astype(np.uint64))
+        if l.size <= cap:
+            counts.copy_(torch.from_numpy(np.diff(o).astype(np.int32)))
+            locs[:l.size].copy_(torch.from_numpy(l.astype(np.int32)))
+        return int(l.size)
+
+    sl = D.ShardedLocate(locate_fn=oracle_locate, dtype=torch.int32)
+    goff, glocs = sl.locate(torch.from_numpy(data), torch.from_numpy(offs))
+    ref_off, ref_locs = ix.locate_batch(data, offs.astype(np.uint64))
+    ok = (np.array_equal(goff.numpy().astype(np.uint64), ref_off)
+          and np.array_equal(glocs.numpy().astype(np.uint32), ref_locs)
+          and sl.last["shard"] == D.shard(len(pats), world, rank))
+    flags = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        with open(result_path, "w") as f:
+            f.write("ok" if int(flags) == 1 else "mismatch")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_locate_gloo(tmp_path, world):
+    """distributed.ShardedLocate: every rank's answer for the whole batch
+    equals the single-process oracle's (short patterns with thousands of
+    occurrences force the second, exactly sized run on some ranks)."""
+    import torch.multiprocessing as mp
+    out = tmp_path / "sharded.txt"
+    mp.spawn(_sharded_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    assert out.read_text() == "ok"
+
+
 def test_shard_partition(pkg):
     for n in (0, 1, 7, 100, 1001):
         for w in (1, 2, 3, 8):
