@@ -213,3 +213,40 @@ def test_load_file_threaded_ring(pkg, O, tmp_path):
         got = f.locate_batch(pats)
         assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), f"chunk {chunk}"
         f.close()
+
+
+C_HOST = os.path.join(ROOT, "sview-fmindex_amd", "lib", "fmx_locate")
+
+
+def test_c_host_links_and_reports_abi(pkg):
+    """examples/fmx_locate.c (built by build()) links against libfmx.so and
+    agrees on the ABI version — no GPU call."""
+    import subprocess
+    if not os.path.exists(C_HOST):
+        import __graft_entry__ as g
+        g.build_c_host()
+    p = subprocess.run([C_HOST, "--abi"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and p.stdout.strip() == "fmx ABI 4"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("block2", [False, True])
+def test_c_host_locate_matches_oracle(pkg, O, tmp_path, block2):
+    """The C host locates a pattern file against a blob file and writes the
+    reference bench's results format; the file equals the oracle's answer."""
+    import subprocess
+    d = str(tmp_path)
+    cli.generate_text(d, 200_000, 3, True)
+    cli.generate_pattern(d, 20, 3000, 1.0, 3, True)
+    with open(os.path.join(d, "pattern.txt"), "ab") as f:
+        f.write(b"\nA\nNNNN\nacgtACGT\r\nTTTTTTTTTTTTTTTTTTTTTTTTTTTTTT\n")
+    blob_path = cli.build(d, "sview-memory", 2, 3, block2)[0]
+    out = os.path.join(d, "c-results.txt")
+    args = [C_HOST, blob_path, os.path.join(d, "pattern.txt"), out] + (["--block2"] if block2 else [])
+    p = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    assert "Blob loading time:" in p.stdout and "Locate processing time:" in p.stdout
+    planes = 2 if block2 else 3
+    want = _oracle_results(O, np.fromfile(blob_path, np.uint8), planes,
+                           cli.read_patterns(os.path.join(d, "pattern.txt")))
+    assert open(out, "rb").read() == want
