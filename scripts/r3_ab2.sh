@@ -10,6 +10,8 @@ run() {  # name, dir, args...
   local name=$1 dir=$2; shift 2
   ( cd $dir && timeout -k 10 300 python -u bench.py "$@" ) > $O/$name.json 2> $O/$name.err || exit 1
 }
+FMX_SEARCH_PERSISTENT=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_gpu.py -k "group or queue or fixed_len or split_timers" > $O/persistent_pytest.log 2>&1 || exit 1
 for i in 1 2 3; do
   run c1_r2_$i ab_r2 --config c1 --no-derived --no-cpu || exit 1
   run c1_r3_$i . --config c1 --no-cpu --no-blob-layout || exit 1

@@ -401,6 +401,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     if (hipMemset(ix->d_status, 0, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     ix->slots.assign(kStatusSlots, StatusSlot{});
+    if (const char *e = getenv("FMX_SEARCH_PERSISTENT")) ix->search_persistent = e[0] == '1';
     for (uint32_t i = kStatusSlots; i-- > 0;) ix->free_slots.push_back(i);
     {
         int idx = -1;
@@ -940,6 +941,10 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
             stage |= j.flags & FMX_HINT_LONG_PATTERNS;
         }
         if (grp.n == 0) continue;
+        // (A/B) the persistent grid's tile counter: batch 0's workspace header
+        if (ix->search_persistent && ix->occ_mode == FMX_OCC_INTERLEAVED && !ix->qa.dlut && !ix->qa.safull &&
+            !ix->qa.text)
+            grp.tile_ctr = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - 256);
         const fmx_status st = dev_err(timed_split(ix, "locate", "locate.search", "locate.emit", s, units,
                                                   [&](hipEvent_t mid) {
             return launch_locate_group(ix, grp, stage, status, s, mid);

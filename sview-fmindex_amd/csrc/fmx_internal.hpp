@@ -145,6 +145,7 @@ struct fmx_index {
     std::vector<uint32_t> free_slots;
     uint64_t status_clock = 0;
     bool status_pressure = false;  // most words assigned: launches record completion events
+    bool search_persistent = false;  // FMX_SEARCH_PERSISTENT=1: k_search on a resident-sized grid (A/B)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -199,6 +200,10 @@ struct LocateGroup {
     LocateBatch b[kMaxGroup];
     uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
     uint32_t n;
+    // FMX_SEARCH_PERSISTENT=1 (A/B): k_search runs a resident-sized grid whose
+    // workgroups take tiles from this counter (batch 0's workspace header,
+    // zero between launches: k_emit resets it); null = one workgroup per tile
+    uint32_t *tile_ctr;
 };
 // `mid` (optional): an event recorded between k_search and k_emit (timing).
 hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,

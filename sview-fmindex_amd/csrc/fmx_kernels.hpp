@@ -352,6 +352,29 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search(
     search_tile<P, N, VB, REC, VAR>(a, grp, s, s_pat, s_scan, stage_bytes, blockIdx.x);
 }
 
+// The same on a resident-sized grid (FMX_SEARCH_PERSISTENT=1, A/B): each
+// workgroup stages the tables once, then takes 256-pattern tiles from an
+// atomic counter until none is left; no workgroup waits on another.
+template <typename P, int N, int VB, int REC, int VAR>
+__global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_tiles(const QueryArgs a,
+                                                                                      const LocateGroup grp,
+                                                                                      uint32_t stage_bytes,
+                                                                                      uint32_t tiles) {
+    __shared__ Tables<P> s;
+    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    __shared__ uint64_t s_scan[4];
+    __shared__ uint32_t s_tile;
+    stage_tables(a, s, s_pat + stage_bytes);
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(grp.tile_ctr, 1u);
+        __syncthreads();  // (also publishes the tables on the first pass)
+        const uint32_t vt = s_tile;
+        if (vt >= tiles) break;
+        // (search_tile's closing barriers order every read of s_tile before the next write)
+        search_tile<P, N, VB, REC, VAR>(a, grp, s, s_pat, s_scan, stage_bytes, vt);
+    }
+}
+
 // 3. Output offsets (tile offset + in-tile scan) and every location, rows
 // dealt across each wave's lanes (emit_locations).
 // fold: batches of at most kFoldTiles tiles need no k_scan: each workgroup
@@ -400,6 +423,7 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
         *B.needed = base + agg;
     }
     if (i < npat) B.loc_off[i] = my_off;
+    if (grp.tile_ctr && blockIdx.x == 0 && threadIdx.x == 0) *grp.tile_ctr = 0u;  // (k_search is done with it)
     emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, B.cap,
                                   reinterpret_cast<P *>(B.out_locs));
 }

@@ -76,7 +76,18 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
                      uint32_t tiles, uint32_t sb, hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
         const uint32_t lds = sb + qa.kt_lds_bytes;
-        if (var == kVarFaithful) {
+        if (var == kVarFaithful && grp.tile_ctr) {
+            // resident-sized grid: workgroups per CU at this LDS size x CUs
+            int per_cu = 0, dev = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_search_tiles<P, N, VB, R, kVarFaithful>, 256,
+                                                             lds) != hipSuccess ||
+                hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                return hipErrorInvalidValue;
+            const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)std::max(1, per_cu * cus));
+            hipLaunchKernelGGL((k_search_tiles<P, N, VB, R, kVarFaithful>), dim3(grid), dim3(256), lds, s, qa, grp, sb,
+                               tiles);
+        } else if (var == kVarFaithful) {
             hipLaunchKernelGGL((k_search<P, N, VB, R, kVarFaithful>), dim3(tiles), dim3(256), lds, s, qa, grp, sb);
         } else if constexpr (faithful_only(R)) {
             return hipErrorInvalidValue;
