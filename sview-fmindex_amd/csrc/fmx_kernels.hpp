@@ -365,7 +365,7 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
     __shared__ uint64_t s_scan[4];
     __shared__ uint32_t s_tile;
     stage_tables(a, s, s_pat + stage_bytes);
-    for (;;) {
+    for (uint32_t it = 0; it < tiles; ++it) {  // (at most every tile: the loop always ends)
         if (threadIdx.x == 0) s_tile = atomicAdd(grp.tile_ctr, 1u);
         __syncthreads();  // (also publishes the tables on the first pass)
         const uint32_t vt = s_tile;
