@@ -365,10 +365,13 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
     __shared__ uint64_t s_scan[4];
     __shared__ uint32_t s_tile;
     stage_tables(a, s, s_pat + stage_bytes);
-    for (uint32_t it = 0; it < tiles; ++it) {  // (at most every tile: the loop always ends)
+    // Bounded, with a wave-uniform (scalar) exit: an unbounded for (;;) whose
+    // only exit was a branch on the LDS value hung on the GPU (the compiler
+    // cannot prove that branch uniform around the barriers).
+    for (uint32_t it = 0; it < tiles; ++it) {
         if (threadIdx.x == 0) s_tile = atomicAdd(grp.tile_ctr, 1u);
         __syncthreads();  // (also publishes the tables on the first pass)
-        const uint32_t vt = s_tile;
+        const uint32_t vt = __builtin_amdgcn_readfirstlane(s_tile);
         if (vt >= tiles) break;
         // (search_tile's closing barriers order every read of s_tile before the next write)
         search_tile<P, N, VB, REC, VAR>(a, grp, s, s_pat, s_scan, stage_bytes, vt);
