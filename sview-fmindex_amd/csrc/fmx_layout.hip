@@ -5,9 +5,6 @@
 // occ record encoding (blob layout, 64-B or
 // 128-B interleaved records: plain, paired-chunk or symbol-mask) are dispatched
 // at run time.
-#include <cstdio>
-#include <cstdlib>
-
 #include "fmx_kernels.hpp"
 
 #if !defined(FMX_LAYOUT_P) || !defined(FMX_LAYOUT_N) || !defined(FMX_LAYOUT_VB)
@@ -87,11 +84,7 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
                 hipGetDevice(&dev) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
                 return hipErrorInvalidValue;
-            uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)std::max(1, per_cu * cus));
-            if (const char *g = getenv("FMX_SEARCH_GRID")) grid = std::min<uint32_t>(tiles, (uint32_t)atoi(g));
-            if (getenv("FMX_SEARCH_DEBUG"))
-                fprintf(stderr, "[k_search_tiles] tiles %u per_cu %d cus %d grid %u lds %u ctr %p\n", tiles, per_cu,
-                        cus, grid, lds, (void *)grp.tile_ctr);
+            const uint32_t grid = std::min<uint32_t>(tiles, (uint32_t)std::max(1, per_cu * cus));
             hipLaunchKernelGGL((k_search_tiles<P, N, VB, R, kVarFaithful>), dim3(grid), dim3(256), lds, s, qa, grp, sb,
                                tiles);
         } else if (var == kVarFaithful) {
