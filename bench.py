@@ -77,8 +77,10 @@ ACGTN = [b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"]
 AMINO = b"ACDEFGHIKLMNPQRSTVWY"
 CONFIGS = {
     # BASELINE.json configs[0]: the reference's CPU-runnable plumbing case (T is the wildcard)
+    # (1,000-pattern batches: launch-bound, so 16 batches per launch and 8 streams in flight —
+    # 1.46e9 vs 0.66e9 at 8 x 2, profiles/r3/r3c1_sweep.txt)
     "c1": dict(text_len=1_000_000, alphabet=b"ACGT", symbols=[b"Aa", b"Cc", b"Gg", b"Tt"], pos=4, planes=2,
-               vec=64, k=3, sr=2, patterns=1_000, m=20, total=0,
+               vec=64, k=3, sr=2, patterns=1_000, m=20, total=0, group=16, streams=8,
                desc="C1: 1 Mbp ACGT, 1,000 x 20 bp, u32/Block2<u64>, sr 2, k 3"),
     # configs[1]: the headline (metric quoted on it)
     "c2": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
@@ -136,9 +138,9 @@ def parse():
     ap.add_argument("--no-fixed-len", action="store_true",
                     help="A/B: do not pass FMX_HINT_FIXED_LEN (the kernels read each tile's offsets first)")
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--streams", type=int, default=2, help="launches in flight (HIP streams)")
+    ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
     ap.add_argument("--batches", type=int, default=32, help="distinct batches cycled (weak-scaling configs)")
-    ap.add_argument("--group", type=int, default=8, help="batches per kernel launch (at most 16)")
+    ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 16; default 8, c1: 16)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment (weak configs): each launch group's patterns arranged so that workgroup "
@@ -460,8 +462,8 @@ def main():
     B = args.patterns or cfg["patterns"]
     total = args.total_patterns if args.total_patterns >= 0 else cfg["total"]
     P = cfg["pos"]
-    S = max(1, args.streams)
-    GR = max(1, min(args.group, 16))
+    S = max(1, args.streams or cfg.get("streams", 2))
+    GR = max(1, min(args.group or cfg.get("group", 8), 16))
     BLK = cfg["planes"] * cfg["vec"] // 8
     position = pkg.u32 if P == 4 else pkg.u64
     block = getattr(pkg.blocks, f"Block{cfg['planes']}")(pkg.Vector(cfg["vec"]))
