@@ -141,6 +141,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
     ap.add_argument("--batches", type=int, default=32, help="distinct batches cycled (weak-scaling configs)")
     ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 16; default 8, c1: 16)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one pass (every launch, forked over the streams) in a HIP graph and replay it: "
+                         "one host call per pass instead of one per launch (launch-bound configs)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment (weak configs): each launch group's patterns arranged so that workgroup "
@@ -352,6 +355,61 @@ def timed_passes(torch, dist, dist_on, w, launches, warmup, min_seconds, event_e
         dist.barrier()
     ix.timing_enable(False)
     return elapsed, passes, count[0] // passes, count[1] // passes, ix.timing_read()
+
+
+def capture_pass(torch, w, launches):
+    """One pass — `launches` launches, group q on its own stream q % S — captured
+    in a HIP graph: the other streams fork from the first and join it at the
+    end, so the replay keeps the launches' concurrency.  The engine's launch
+    path is capture-safe (no synchronous call; timing must be off)."""
+    g = torch.cuda.CUDAGraph()
+    s0 = w.streams[0]
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s0):
+        fork = torch.cuda.Event()
+        fork.record(s0)
+        for st in w.streams[1:]:
+            st.wait_event(fork)
+        w.cursor = 0
+        for _ in range(launches):
+            w.launch_next()
+        for st in w.streams[1:]:
+            join = torch.cuda.Event()
+            join.record(st)
+            s0.wait_event(join)
+    w.cursor = 0
+    return g
+
+
+def timed_graph(torch, dist, dist_on, w, launches, warmup, min_seconds):
+    """timed_passes with every pass a replay of one captured graph."""
+    for q in range(max(warmup, w.n_groups)):
+        w.launch(q % w.n_groups)
+    torch.cuda.synchronize()
+    w.check_capacity()
+    w.ix.timing_enable(False)
+    g = capture_pass(torch, w, launches)
+    per = sum(w.groups[q % w.n_groups]["patterns"] for q in range(launches))
+    nbat = sum(len(w.groups[q % w.n_groups]["batches"]) for q in range(launches))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    passes = max(1, math.ceil(1.3 * min_seconds / max(time.perf_counter() - t0, 1e-6)))
+    if dist_on:
+        pt = torch.tensor([passes], dtype=torch.int64, device="cuda")
+        dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        passes = int(pt.item())
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        g.replay()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        dist.barrier()
+    return elapsed, passes, nbat, per, {}
 
 
 def kernel_pass(torch, w, launches):
@@ -573,8 +631,12 @@ def main():
         w.rebind([(jg.counts_slot(k), jg.locs_slot(k)) for k in range(len(w.batches))])
 
     # ---- timed region: compute ----------------------------------------------
-    elapsed, passes, per_pass, pats_pass, timing = timed_passes(torch, dist, dist_on, w, launches, args.warmup,
-                                                                args.min_seconds, args.event_every)
+    if args.graph:
+        elapsed, passes, per_pass, pats_pass, timing = timed_graph(torch, dist, dist_on, w, launches, args.warmup,
+                                                                   args.min_seconds)
+    else:
+        elapsed, passes, per_pass, pats_pass, timing = timed_passes(torch, dist, dist_on, w, launches, args.warmup,
+                                                                    args.min_seconds, args.event_every)
     if dist_on:
         elapsed = D.max_over_ranks(elapsed, device=dev)
     # every pattern a launch ran counts (a pass of K steps runs ceil(K / GR) whole launches)
@@ -757,6 +819,7 @@ def main():
             "index_hbm_bytes": blob_len + info["device_bytes"],
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
             "streams": S, "fixed_len_hint": fixed, "batches_per_launch": GR, "distinct_batches": len(w.batches),
+            "hip_graph": bool(args.graph),
         },
         "roofline": roof,
         "kernels_ms_per_launch_timed_region": per_launch_ms(timing),
