@@ -753,7 +753,7 @@ def main():
     tr = traffic_of(args.traffic_json, key)
     roof = {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": tr["hbm_bytes_per_launch"] if tr else None,
+        "traffic": tr["fabric_bytes_per_launch"] if tr else None,
         "achieved_basis": "per-step cost: the reference algorithm's bytes per pattern (SURVEY.md 8(d), "
                           "alg_bytes_per_pattern) x the timed region's patterns/s per GPU",
         "alg_bytes_per_pattern": alg_per_pattern,
@@ -769,8 +769,8 @@ def main():
         },
     }
     if tr:
-        req = tr.get("hbm_requests_per_launch")
-        tpp = tr["hbm_bytes_per_launch"] / tr.get("patterns_per_launch", ppl or 1)
+        req = tr.get("fabric_requests_per_launch")
+        tpp = tr["fabric_bytes_per_launch"] / tr.get("patterns_per_launch", ppl or 1)
         roof.update({
             "traffic_what": "memory-side (fabric) read bytes per launch: TCC_EA0_RDREQ requests x their size; on "
                             "gfx950 these include Infinity Cache hits (MI355X_MICROARCH.md, HBM section), so "

@@ -8,7 +8,9 @@ FETCH_SIZE (KB) is the L2's memory-side read bytes (TCC_EA0_RDREQ x 64 B per
 request on gfx950, MI355X_MICROARCH.md HBM section); the request split into
 64-B and 128-B requests comes from TCC_EA0_RDREQ_64B/_128B, so the bytes
 actually requested are 64 n64 + 128 n128 (+ 32 n32) — reported as
-hbm_bytes_per_launch, with FETCH_SIZE kept alongside."""
+fabric_bytes_per_launch (memory-side requests: on gfx950 they include
+Infinity Cache hits, so they bound the HBM bytes from above), with
+FETCH_SIZE kept alongside."""
 import csv
 import json
 import os
@@ -59,14 +61,14 @@ def main():
         "tag": tag, "source": "rocprofv3 --pmc, scripts/r2_profile.sh + scripts/traffic.py",
         "launches_profiled": nl, "patterns_per_launch": ppl,
         "fetch_size_bytes_per_launch": fetch["FETCH_SIZE"] * 1024 / nl,
-        "hbm_requests_per_launch": nreq, "requests_32b": n32, "requests_64b": n64, "requests_128b": n128,
-        "hbm_bytes_per_launch": 32 * n32 + 64 * n64 + 128 * n128,
+        "fabric_requests_per_launch": nreq, "requests_32b": n32, "requests_64b": n64, "requests_128b": n128,
+        "fabric_bytes_per_launch": 32 * n32 + 64 * n64 + 128 * n128,
         "write_bytes_per_launch": wr["WRITE_SIZE"] * 1024 / nl3,
         "l2_hit_rate": tcc["TCC_HIT_sum"] / max(tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"], 1),
         "l2_requests_per_pattern": (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]) / nl4 / ppl,
     }
-    run["hbm_bytes_per_pattern"] = run["hbm_bytes_per_launch"] / ppl
-    run["hbm_requests_per_pattern"] = nreq / ppl
+    run["fabric_bytes_per_pattern"] = run["fabric_bytes_per_launch"] / ppl
+    run["fabric_requests_per_pattern"] = nreq / ppl
     db = json.load(open(out)) if os.path.exists(out) else {"runs": {}}
     db.setdefault("runs", {})[key] = run
     json.dump(db, open(out, "w"), indent=1, sort_keys=True)
