@@ -276,6 +276,33 @@ fmx_status fmx_sync(fmx_index *ix, void *stream);
  * (or sync) a stream before destroying it. */
 fmx_status fmx_stream_release(fmx_index *ix, void *stream);
 
+/* ----------------------------------------------------- several GPUs, one handle
+ * The device mask of SURVEY §8(b) for a single-process caller (no process
+ * group): one replica of the index per entry of `devices` (a device may be
+ * listed more than once: replicas on one GPU run concurrently).  The blob is
+ * validated like fmx_load (same codes), copied to HBM of devices[0] once and
+ * from there device-to-device to the other replicas (hipMemcpyPeer: xGMI
+ * between MI355X GPUs); each replica is an fmx_load_device index.  A host
+ * batch is cut into n_replicas contiguous shards (sizes differ by at most
+ * one) answered concurrently, and the results are concatenated in order:
+ * exactly what fmx_count_batch / fmx_locate_batch on one device return for
+ * the whole batch (same capacity contract: offsets and *needed are written,
+ * FMX_E_CAPACITY if the total exceeds cap). */
+typedef struct fmx_multi fmx_multi;
+
+fmx_status fmx_multi_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, const int *devices,
+                          int n_devices, uint32_t options, fmx_multi **out, uint64_t *expected_total,
+                          uint64_t *actual_total);
+void fmx_multi_free(fmx_multi *m);
+int fmx_multi_replicas(const fmx_multi *m);
+/* Replica i's own index (for the device-buffer calls on its device); owned by m. */
+fmx_index *fmx_multi_replica(fmx_multi *m, int i);
+fmx_status fmx_multi_count_batch(fmx_multi *m, const uint8_t *bytes, const uint64_t *offsets,
+                                 uint64_t n_patterns, uint32_t flags, void *out_counts);
+fmx_status fmx_multi_locate_batch(fmx_multi *m, const uint8_t *bytes, const uint64_t *offsets,
+                                  uint64_t n_patterns, uint32_t flags, uint64_t *out_loc_offsets,
+                                  void *out_locs, uint64_t cap, uint64_t *needed);
+
 /* --------------------------------------------------------------- timing
  * enable = k > 0: every k-th kernel launch (k = 1: every launch) is bracketed
  * by hipEvents on its stream; 0: off.  fmx_timing_read sums the bracketed

@@ -615,6 +615,83 @@ class FmIndex:
                                        "units": arr[i].units} for i in range(min(cnt.value, 16))}
 
 
+# ------------------------------------------------------- MultiDeviceIndex
+
+class MultiDeviceIndex:
+    """One index over several GPUs of this process (fmx_multi_*): a replica
+    per entry of `devices` (the blob copied host -> devices[0] once, then
+    device to device), batches cut into contiguous shards answered
+    concurrently and concatenated — the same answers as `FmIndex` on one
+    device, for a single-process caller with no process group."""
+
+    def __init__(self, blob, devices: Sequence[int], position: Position = u32, block: Optional[_Block] = None,
+                 text_encoder=text_encoders.EncodingTable, options: int = _n.FMX_OPT_DEFAULT):
+        block = block or blocks.Block2(Vector.U64)
+        if isinstance(text_encoder, type):
+            text_encoder = text_encoder.__new__(text_encoder)
+        arr = blob if isinstance(blob, np.ndarray) else np.frombuffer(bytes(blob), dtype=np.uint8)
+        if arr.ctypes.data % block.ALIGN_SIZE:
+            a2 = aligned_buffer(arr.size, 16)
+            a2[:] = arr
+            arr = a2
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        exp, act = C.c_uint64(), C.c_uint64()
+        st = _n.lib().fmx_multi_load(_ptr(arr), arr.size, _layout(position, block, text_encoder), devs, len(devices),
+                                     options, C.byref(h), C.byref(exp), C.byref(act))
+        if st == _n.FMX_E_FORMAT:
+            raise InvalidFormat()
+        if st == _n.FMX_E_SIZE:
+            raise MismatchedBlobSize(exp.value, act.value)
+        _check(st, "fmx_multi_load")
+        self._h = h
+        self._dt = position.dtype
+        self.devices = list(devices)
+
+    @property
+    def replicas(self) -> int:
+        return _n.lib().fmx_multi_replicas(self._h)
+
+    def close(self):
+        if self._h:
+            _n.lib().fmx_multi_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def count_batch(self, patterns, reversed: bool = False) -> np.ndarray:
+        data, offsets = patterns if isinstance(patterns, tuple) else pack_patterns(patterns)
+        n = offsets.size - 1
+        out = np.zeros(max(n, 1), dtype=self._dt)
+        flags = _n.FMX_PATTERN_REVERSED if reversed else 0
+        _check(_n.lib().fmx_multi_count_batch(self._h, _ptr(data) if data.size else None, _ptr(offsets), n, flags,
+                                              _ptr(out)), "fmx_multi_count_batch")
+        return out[:n]
+
+    def locate_batch(self, patterns, reversed: bool = False,
+                     cap: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+        data, offsets = patterns if isinstance(patterns, tuple) else pack_patterns(patterns)
+        n = offsets.size - 1
+        loc_off = np.zeros(n + 1, dtype=np.uint64)
+        flags = _n.FMX_PATTERN_REVERSED if reversed else 0
+        needed = C.c_uint64()
+        cap = (1 << 16) if cap is None else cap
+        locs = np.zeros(max(cap, 1), dtype=self._dt)
+        args = lambda: (self._h, _ptr(data) if data.size else None, _ptr(offsets), n, flags, _ptr(loc_off),  # noqa
+                        _ptr(locs), cap, C.byref(needed))
+        st = _n.lib().fmx_multi_locate_batch(*args())
+        if st == _n.FMX_E_CAPACITY:
+            cap = needed.value
+            locs = np.zeros(max(cap, 1), dtype=self._dt)
+            st = _n.lib().fmx_multi_locate_batch(*args())
+        _check(st, "fmx_multi_locate_batch")
+        return loc_off, locs[:needed.value]
+
+
 # ---------------------------------------------------------- FmIndexBuilder
 
 class FmIndexBuilder:

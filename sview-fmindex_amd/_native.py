@@ -92,6 +92,12 @@ SIGNATURES = {
     "fmx_locate_group_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64, _p]),
     "fmx_sync": (_i, [_p, _p]),
     "fmx_stream_release": (_i, [_p, _p]),
+    "fmx_multi_load": (_i, [_p, _u64, fmx_layout, C.POINTER(_i), _i, _u32, C.POINTER(_p), _PU64, _PU64]),
+    "fmx_multi_free": (None, [_p]),
+    "fmx_multi_replicas": (_i, [_p]),
+    "fmx_multi_replica": (_p, [_p, _i]),
+    "fmx_multi_count_batch": (_i, [_p, _p, _p, _u64, _u32, _p]),
+    "fmx_multi_locate_batch": (_i, [_p, _p, _p, _u64, _u32, _p, _p, _u64, _PU64]),
     "fmx_timing_enable": (_i, [_p, _i]),
     "fmx_timing_read": (_i, [_p, C.POINTER(fmx_kernel_timing), _i, C.POINTER(_i)]),
     "fmx_build_blob_size": (_i, [_u64, _u32, fmx_layout, _u32, _u32, _PU64]),

@@ -84,6 +84,13 @@ def test_load_rejects_bad_blobs_before_touching_the_device(pkg, O):
     # P/B/E are not in the blob: a wrong layout tag is caught by the consistency checks
     with pytest.raises((pkg.LoadError, pkg.FmxError)):
         pkg.FmIndex.load(blob, pkg.u64, pkg.blocks.Block2(pkg.Vector.U64))
+    # the multi-device handle validates the same way, before any device
+    with pytest.raises(pkg.LoadError.InvalidFormat):
+        pkg.MultiDeviceIndex(bad, [0, 1], pkg.u32, pkg.blocks.Block2(pkg.Vector.U64))
+    with pytest.raises(pkg.LoadError.MismatchedBlobSize):
+        pkg.MultiDeviceIndex(longer, [0], pkg.u32, pkg.blocks.Block2(pkg.Vector.U64))
+    with pytest.raises(pkg.FmxError):
+        pkg.MultiDeviceIndex(blob, [], pkg.u32, pkg.blocks.Block2(pkg.Vector.U64))
 
 
 def test_pack_patterns(pkg):
