@@ -247,6 +247,8 @@ class Workload:
         self.n_groups = -(-len(self.batches) // GR)
         self.bind()
         self.cursor = 0
+        # the batches were made on torch's stream; the launches use self.streams
+        torch.cuda.synchronize()
 
     def bind(self):
         """(Re)build each launch group's job queue from the batches' current buffers."""
@@ -266,6 +268,7 @@ class Workload:
         for bt, (c, l) in zip(self.batches, outputs):
             bt["cnt"], bt["locs"], bt["cap"] = c, l, int(l.numel())
         self.bind()
+        self.torch.cuda.synchronize()
 
     def launch(self, g, stream=None):
         grp = self.groups[g]

@@ -180,10 +180,13 @@ class ShardedLocate:
     every rank and equal to one device's answer for the whole batch.
 
     `locate_fn(d_bytes, d_offsets, m, counts_out, locs_out, cap) -> needed`
-    runs the shard (FmIndex by default: fmx_locate_batch_async on `stream`);
-    if the shard has more occurrences than the first guess of room, it runs
-    again with exactly enough.  Host round trips per call: the shard's byte
-    range, its location total and the size exchange."""
+    runs the shard (FmIndex by default: fmx_locate_batch_async on `stream`,
+    else on the caller's current stream — the stream the shard's inputs and
+    output buffers were made on, so the launch is ordered after them; a
+    given stream first waits for the current one); if the shard has more
+    occurrences than the first guess of room, it runs again with exactly
+    enough.  Host round trips per call: the shard's byte range, its location
+    total and the size exchange."""
 
     def __init__(self, ix=None, dtype=None, device=None, group=None, locate_fn=None, stream=None):
         import torch
@@ -205,7 +208,10 @@ class ShardedLocate:
             self._ws = torch.zeros(ws, dtype=torch.uint8, device=d_offsets.device)
         loff = torch.zeros(m + 1, dtype=torch.int64, device=d_offsets.device)
         need = torch.zeros(1, dtype=torch.int64, device=d_offsets.device)
-        st = self.stream.cuda_stream if self.stream is not None else 0
+        cur = torch.cuda.current_stream(d_offsets.device)
+        if self.stream is not None:  # ordered after everything the current stream made
+            self.stream.wait_stream(cur)
+        st = (self.stream or cur).cuda_stream
         self.ix.locate_batch_async(d_bytes.data_ptr() if d_bytes.numel() else 0, d_offsets.data_ptr(), m,
                                    loff.data_ptr(), locs.data_ptr() if cap else 0, cap, need.data_ptr(),
                                    self._ws.data_ptr(), self._ws.numel(), d_counts=counts.data_ptr() if m else 0,

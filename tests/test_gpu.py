@@ -308,6 +308,7 @@ def test_device_async_api(pkg, O):
     d_need = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = ix.locate_workspace_size(n)
     d_ws = torch.zeros(ws, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # (buffers made on torch's stream; the index launches on its own)
     ix.locate_batch_async(d_data.data_ptr(), d_off.data_ptr(), n, d_loff.data_ptr(), d_locs.data_ptr(), cap,
                           d_need.data_ptr(), d_ws.data_ptr(), ws, d_counts=d_cnt.data_ptr())
     ix.sync()
@@ -494,6 +495,7 @@ def test_locate_queue_many_launches_one_workspace(pkg, O):
         jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), b["n"], b["loff"][k].data_ptr(),
                                   b["locs"][k].data_ptr(), b["cap"], b["need"].data_ptr(), d_ws.data_ptr(), ws))
     q = ix.job_queue(jobs)
+    torch.cuda.synchronize()  # (buffers made on torch's stream; the index launches on its own)
     for rep in range(2):
         ix.locate_jobs_async(q)
         ix.sync()
@@ -542,6 +544,7 @@ def test_locate_group_launch(pkg, O):
         bats.append(b)
     q = ix.job_queue(jobs)
     stream = torch.cuda.Stream(device=dev)
+    torch.cuda.synchronize()  # (buffers made on torch's stream; the launches use another)
     for rep in range(70):
         ix.locate_group_async(q, stream=stream.cuda_stream)
     ix.sync(stream.cuda_stream)
@@ -620,6 +623,7 @@ def test_fixed_len_hint(pkg, O, m):
         jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), n, b["loff"].data_ptr(),
                                   b["locs"].data_ptr(), cap, b["need"].data_ptr(), b["ws"].data_ptr(), ws,
                                   d_counts=b["cnt"].data_ptr(), reversed=rev, stage_kb=stage_kb, fixed_len=m))
+        torch.cuda.synchronize()  # (buffers made on torch's stream; the index launches on its own)
         ix.count_batch_async(b["data"].data_ptr(), b["off"].data_ptr(), n, b["cnt2"].data_ptr(),
                              reversed=rev, stage_kb=stage_kb, fixed_len=m)
         bats.append(b)
@@ -745,12 +749,12 @@ def test_status_slots_recycled(pkg, O):
         streams.append(lost)
         ix.count_batch_async(bd.data_ptr(), bo.data_ptr(), 11, bc.data_ptr(), stream=lost)
         torch.cuda.synchronize()
+        outs = [torch.zeros(len(pats), dtype=torch.int32, device=dev) for _ in range(2300)]
+        torch.cuda.synchronize()  # (made on torch's stream; the launches use raw streams)
         for i in range(2300):
             s = new_stream()
             streams.append(s)
-            c = torch.zeros(len(pats), dtype=torch.int32, device=dev)
-            ix.count_batch_async(d.data_ptr(), o.data_ptr(), len(pats), c.data_ptr(), stream=s)
-            outs.append(c)
+            ix.count_batch_async(d.data_ptr(), o.data_ptr(), len(pats), outs[i].data_ptr(), stream=s)
             if i % 97 == 0:
                 ix.sync(s)
         torch.cuda.synchronize()
@@ -771,6 +775,7 @@ def test_status_slots_recycled(pkg, O):
         assert e.value.code == pkg._native.FMX_E_EMPTY_PATTERN
         ix.sync(r)
         c = torch.zeros(len(pats), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
         ix.count_batch_async(d.data_ptr(), o.data_ptr(), len(pats), c.data_ptr(), stream=r)
         ix.release_stream(r)
         assert np.array_equal(c.cpu().numpy().view(np.uint32), want)
@@ -802,6 +807,7 @@ def test_locate_split_timers(pkg, O):
     ws = torch.zeros(ix.locate_workspace_size(n), dtype=torch.uint8, device=dev)
     q = ix.job_queue([ix.locate_job(data.data_ptr(), off.data_ptr(), n, loff.data_ptr(), locs.data_ptr(), 4 * n,
                                     need.data_ptr(), ws.data_ptr(), ws.numel(), fixed_len=m)])
+    torch.cuda.synchronize()  # (the buffers were made on torch's stream; the index launches on its own)
     ix.timing_enable(True)
     for _ in range(6):
         ix.locate_group_async(q)
