@@ -213,7 +213,10 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
  * Asynchronous on `stream` (a hipStream_t; NULL = the index's own stream).
  * Inputs and outputs live in HBM of the index's device.  Errors detected on
  * the device (empty pattern, PassThrough symbol) are latched in a status word
- * read by fmx_sync(). */
+ * read by fmx_sync().  Only `stream` orders the launch: the index's own
+ * stream is non-blocking (not ordered with the caller's streams, nor with the
+ * legacy default stream), so buffers written on another stream must be
+ * complete first — pass the writers' stream, or synchronise. */
 
 fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets,
                                  uint64_t n_patterns, uint32_t flags, void *d_counts, void *stream);
