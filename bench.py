@@ -152,6 +152,8 @@ def parse():
     ap.add_argument("--presorted", action="store_true",
                     help="experiment (weak configs): each launch group's patterns pre-sorted by reversed "
                          "suffix (upper bound of the cache reuse a suffix sort would buy; not a valid headline)")
+    ap.add_argument("--presort-symbols", type=int, default=14,
+                    help="--presorted: the sort key is the last this many symbols (order within a key kept)")
     return ap.parse_args()
 
 
@@ -615,7 +617,7 @@ def main():
     else:
         w = Workload(torch, ix, d_text, m, weak_starts(NB), P, S, GR, fixed, dev)
         if args.presorted or args.xcd_partitioned:
-            arrange(torch, w, B, m, GR, dev, args.presorted)
+            arrange(torch, w, B, m, GR, dev, args.presorted, args.presort_symbols)
         steps = args.steps or 800
         launches = -(-steps // GR)
     torch.cuda.synchronize()
@@ -970,7 +972,7 @@ def main():
         dist.destroy_process_group()
 
 
-def arrange(torch, w, B, m, GR, dev, presorted):
+def arrange(torch, w, B, m, GR, dev, presorted, key_symbols=14):
     """Experiments (weak configs, uniform batches): rearrange each launch
     group's patterns — sorted by reversed suffix (`presorted`), or so that
     workgroup tile t holds class-(t % 8) patterns (XCD-partitioned)."""
@@ -983,9 +985,9 @@ def arrange(torch, w, B, m, GR, dev, presorted):
             st = torch.cat([b["starts"] for b in sel])
             pats = torch.stack([b["pat"].view(B, m) for b in sel]).view(-1, m).long()
             key = torch.zeros(st.numel(), dtype=torch.int64, device=dev)
-            for q in range(min(m, 14)):
+            for q in range(min(m, key_symbols)):
                 key = key * 4 + code[pats[:, m - 1 - q]]
-            order = torch.argsort(key)
+            order = torch.argsort(key, stable=True)
             st, pats = st[order], pats[order].to(torch.uint8)
             for j, b in enumerate(sel):
                 b["starts"] = st[j * B:(j + 1) * B].contiguous()
