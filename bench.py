@@ -825,6 +825,9 @@ def main():
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
             "streams": S, "fixed_len_hint": fixed, "batches_per_launch": GR, "distinct_batches": len(w.batches),
             "hip_graph": bool(args.graph),
+            "launch_order": (f"grouped by the last {info['group_key_len']} symbols"
+                             if info.get("group_key_len") and B * GR >= info["grouped_min"] and fixed
+                             and m * (table.symbol_count()).bit_length() <= 96 else "as given"),
         },
         "roofline": roof,
         "kernels_ms_per_launch_timed_region": per_launch_ms(timing),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 4u
+#define FMX_ABI_VERSION 5u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -138,6 +138,11 @@ typedef struct fmx_index_info {
     uint32_t occ_record;     /* occ record encoding: 0 blob layout, 64/128 interleaved
                                 records, | 1 paired-chunk, | 2 symbol-mask records
                                                                      */
+    uint32_t group_key_len;  /* grouped launches: the key's last symbols (0: none) */
+    uint32_t group_key_base; /* ... as digits over this many symbols               */
+    uint64_t grouped_min;    /* fixed-length launches of at least this many
+                                patterns are grouped (UINT64_MAX: never, the
+                                default)                                            */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {
@@ -222,10 +227,19 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
                                  uint64_t n_patterns, uint32_t flags, void *d_counts, void *stream);
 
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
- * [256 B][tile counts][tile offsets][one search record per pattern].  A
+ * [256 B][16 KiB of key counters][tile counts][tile offsets][one search
+ * record per pattern][key, place and two 16-B records per pattern].  A
  * workspace is zeroed by the caller before its first use, then belongs to
- * this index: its launches are ordered on one stream at a time.  (A locate is
- * k_search + k_emit, neither of which makes one workgroup wait on another.) */
+ * this index: its launches are ordered on one stream at a time (every launch
+ * leaves the key counters zero again).  A locate is k_search + k_emit.  A
+ * grouped locate (opt-in, environment at load: FMX_GROUPED=1, or
+ * FMX_GROUPED_MIN=<patterns per launch>; fixed-length batches whose
+ * patterns pack into 96 bits, faithful index) first deals its patterns out
+ * in the order of their last symbols, so that patterns whose backward
+ * searches share their first LF steps run side by side, and searches them in
+ * that order — same results; measured slower than launch order on MI355X
+ * (DESIGN.md §5), hence off by default.  No kernel makes one workgroup wait
+ * on another. */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)

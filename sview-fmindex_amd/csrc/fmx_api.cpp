@@ -232,7 +232,13 @@ static hipError_t timed_split(fmx_index *ix, const char *name, const char *first
     return e;
 }
 
-static fmx_status dev_err(hipError_t e) { return e == hipSuccess ? FMX_OK : FMX_E_DEVICE; }
+// FMX_DEBUG=1: name the HIP error behind an FMX_E_DEVICE on stderr
+static fmx_status dev_err(hipError_t e) {
+    if (e == hipSuccess) return FMX_OK;
+    static const bool debug = getenv("FMX_DEBUG") != nullptr;
+    if (debug) fprintf(stderr, "fmx: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
+    return FMX_E_DEVICE;
+}
 
 // Makes the index's device current for one entry point and restores the
 // caller's current device on every return path.
@@ -455,6 +461,20 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
             q.dlut_dig[c] = (uint8_t)S;
             q.dlut_sym[S++] = (uint8_t)c;
         }
+    // grouped launches: the key's digits are these S symbols; as many of the
+    // last symbols as fit kGroupBins bins (C2: 6 of ACGT; C4: 2 residues)
+    ix->gkey_base = S;
+    ix->gkey_len = 0;
+    if (S >= 2)
+        for (uint64_t bins = S; bins <= kGroupBins && ix->gkey_len < 16; bins *= S) ++ix->gkey_len;
+    // off by default: measured slower on every config ("Grouped launches")
+    ix->grouped_min = ~0ull;
+    if (const char *e = getenv("FMX_GROUPED")) {
+        if (e[0] == '0') ix->grouped_min = ~0ull;
+        else if (e[0] == '1') ix->grouped_min = 1;
+    }
+    if (const char *e = getenv("FMX_GROUPED_MIN")) ix->grouped_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("FMX_GROUPED_XCD")) ix->grouped_xcd = e[0] == '1';
     if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
         // the largest K with S^K * 2P <= budget, deeper than the blob's k;
         // budget: FMX_DEEP_LUT_MB, else 160 GiB capped at half the free HBM
@@ -834,6 +854,10 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->context_len = ix->qa.ctx_len;
     o->scan_rows = ix->qa.scan_rows;
     o->occ_record = ix->occ_mode == FMX_OCC_INTERLEAVED ? ix->rec_bytes : 0;
+    const bool faithful = !ix->qa.dlut && !ix->qa.safull && !ix->qa.text && ix->qa.ctx_len == 0;
+    o->group_key_len = faithful ? ix->gkey_len : 0;
+    o->group_key_base = faithful ? ix->gkey_base : 0;
+    o->grouped_min = faithful && ix->gkey_len ? ix->grouped_min : ~0ull;
     o->device = ix->device;
     return FMX_OK;
 }
@@ -852,10 +876,12 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
     });
 }
 
-// Locate workspace: [256 B reserved][tile counts: G][tile offsets: G]
-// [search records: n x locate_rec_bytes(P)], G = ceil(n / 256).
+// Locate workspace (fmx_internal.hpp, kWsHeader): [256 B reserved][group
+// key counters][tile counts: G][tile offsets: G][search records: n x
+// locate_rec_bytes(P)][keys][slots][sorted order], G = ceil(n / 256).
 static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) {
-    return 256 + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes);
+    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes) +
+           ((2 * n + 15) & ~15ull) + ((4 * n + 15) & ~15ull) + 32 * n;
 }
 
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {
@@ -868,7 +894,7 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
                                   uint32_t flags, void *d_counts, uint64_t *d_loc_offsets, void *d_locs,
                                   uint64_t cap, uint64_t *d_needed, void *d_ws, uint64_t ws_bytes, void *stream) {
     if (!ix || !d_loc_offsets || !d_needed || (n && (!d_bytes || !d_offsets)) || (cap && !d_locs)) return FMX_E_ARG;
-    if (!d_ws || ws_bytes < 256 + 16) return FMX_E_ARG;
+    if (!d_ws || ws_bytes < kWsHeader + 16) return FMX_E_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
     DeviceGuard dg(ix->device);
     if (n == 0) {
@@ -882,7 +908,7 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
     return with_status(ix, s, [&](uint32_t *status) {
         return dev_err(timed(ix, "locate", s, n, [&] {
             return launch_locate(ix, d_bytes, d_offsets, n, flags, d_counts, d_loc_offsets, d_locs, cap, d_needed,
-                                 (uint64_t *)(ws + 256), G, status, s);
+                                 (uint64_t *)(ws + kWsHeader), G, status, s);
         }));
     });
 }
@@ -931,7 +957,7 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
             const uint64_t G = locate_tiles_cap(j.n_patterns);
             grp.tile_begin[grp.n] = tiles;
             grp.b[grp.n++] = LocateBatch{j.d_bytes, j.d_offsets, j.n_patterns, j.d_counts, j.d_loc_offsets,
-                                         j.d_locs, j.cap, j.d_needed, (uint64_t *)((uint8_t *)j.d_workspace + 256),
+                                         j.d_locs, j.cap, j.d_needed, (uint64_t *)((uint8_t *)j.d_workspace + kWsHeader),
                                          (j.flags & FMX_PATTERN_REVERSED) ? 1u : 0u, j.flags >> 16};
             tiles += (uint32_t)G;
             units += j.n_patterns;
@@ -944,7 +970,7 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
         // (A/B) the persistent grid's tile counter: batch 0's workspace header
         if (ix->search_persistent && ix->occ_mode == FMX_OCC_INTERLEAVED && !ix->qa.dlut && !ix->qa.safull &&
             !ix->qa.text)
-            grp.tile_ctr = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - 256);
+            grp.tile_ctr = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader);
         const fmx_status st = dev_err(timed_split(ix, "locate", "locate.search", "locate.emit", s, units,
                                                   [&](hipEvent_t mid) {
             return launch_locate_group(ix, grp, stage, status, s, mid);

@@ -146,6 +146,13 @@ struct fmx_index {
     uint64_t status_clock = 0;
     bool status_pressure = false;  // most words assigned: launches record completion events
     bool search_persistent = false;  // FMX_SEARCH_PERSISTENT=1: k_search on a resident-sized grid (A/B)
+    // grouped launches (fmx::kWsHeader), opt-in: launches of at least
+    // grouped_min patterns (FMX_GROUPED_MIN; FMX_GROUPED=1 every launch; the
+    // default never) on the faithful index; the key = the last gkey_len
+    // symbols, digits over the gkey_base symbols that occur in the text
+    uint64_t grouped_min = 0;
+    uint32_t gkey_len = 0, gkey_base = 0;
+    uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -200,6 +207,13 @@ struct LocateGroup {
     LocateBatch b[kMaxGroup];
     uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
     uint32_t n;
+    // Grouped launch (kWsHeader below): the group's key counters (batch 0's
+    // workspace, zero between launches: k_group_tiles re-zeroes them), the
+    // key's symbol count and digit base, the bits per packed symbol, and the
+    // first key/place workgroup of each batch; gcount null = launch order
+    uint32_t *gcount;
+    uint32_t gkey_len, gkey_base, gbits;
+    uint32_t chunk_begin[kMaxGroup];
     // FMX_SEARCH_PERSISTENT=1 (A/B): k_search runs a resident-sized grid whose
     // workgroups take tiles from this counter (batch 0's workspace header,
     // zero between launches: k_emit resets it); null = one workgroup per tile
@@ -212,6 +226,31 @@ hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;
 
+// Grouped launches.  A launch's patterns are searched in the order of their
+// last gkey_len symbols (a counting sort on one key per pattern) instead of
+// the order they were given in, so that patterns whose backward searches
+// share their first LF steps' intervals run in the same wavefronts at the
+// same time and read those occ records once (one request per wave
+// instruction, or an L2 hit) instead of once each.  Results are written at
+// each pattern's own index: identical to a launch in the given order.
+// Fixed-length batches whose patterns pack into 96 bits (gbits per symbol)
+// only: the sorted order carries each pattern's symbols, so that the search
+// reads its patterns in order.
+// Locate workspace of a batch of n patterns (G = ceil(n / 256), R =
+// locate_rec_bytes):
+//   [256 B header][kGroupCounterRoom u32 key counters][tile counts: G][tile
+//   offsets: G][search records: n x R][keys: n x u16][places: n x u32]
+//   (each padded to 16 B)[packed patterns: n x 16 B][sorted order: n x 16 B]
+// The counters sit at a fixed offset so that every launch on a workspace
+// finds them zero whatever its n.
+constexpr uint32_t kGroupKeyBits = 12;
+constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
+constexpr uint32_t kGroupChunkTiles = 8;    // tiles (of 256 patterns) per key workgroup
+constexpr uint32_t kGroupPackBits = 96;
+constexpr uint32_t kGroupCounterRoom = kGroupBins;
+constexpr uint64_t kWsHeader = 256 + 4ull * kGroupCounterRoom;
+inline uint64_t group_chunks(uint64_t n) { return ((n + 255) / 256 + kGroupChunkTiles - 1) / kGroupChunkTiles; }
+
 // The kernels that depend on the occ layout, one table per (P, N) pair
 // (fmx_layout.hip, one translation unit per pair); vb = V bits, rec = 0
 // (blob layout) or the interleaved record bytes, var = search variant
@@ -223,6 +262,9 @@ struct LayoutOps {
                          uint32_t tiles, uint32_t sb, hipStream_t s);
     hipError_t (*emit)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp, uint32_t tiles,
                        uint32_t fold, hipStream_t s);
+    // grouped launch (faithful variant): k_search_grouped over `total` patterns in key order
+    hipError_t (*search_grouped)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
+                                 uint64_t total, uint32_t cap, uint32_t xcd, hipStream_t s);
     hipError_t (*dlut_level)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
                              void *child, hipStream_t s);
     hipError_t (*full_sa)(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t n, void *sa_out,

@@ -378,6 +378,221 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
     }
 }
 
+// ---------------------------------------------------------- grouped launches
+// (fmx_internal.hpp, kWsHeader) k_group_key (one workgroup per chunk of
+// kGroupChunkTiles tiles), k_group_scan and k_group_place deal the launch's
+// patterns out in the order of their keys, each carrying its packed symbols;
+// k_search_grouped searches them in that order and writes each result at
+// the pattern's own index; k_group_tiles sums each tile's counts for k_emit.
+// No workgroup waits on another.
+
+using U4 = uint32_t __attribute__((ext_vector_type(4)));
+
+// A batch's grouping arrays, after its search records.
+struct GroupArrays {
+    uint16_t *keys;
+    uint32_t *slots;      // the pattern's place among the launch's patterns with its key
+    U4 *packed, *sorted;  // {symbols: 96 bits, pattern id}
+};
+__device__ __forceinline__ GroupArrays group_arrays(const LocateBatch &B, uint32_t rec_bytes) {
+    const uint64_t n = B.npat, G = (n + 255) / 256;
+    uint8_t *p = reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + n * rec_bytes;
+    GroupArrays w;
+    w.keys = reinterpret_cast<uint16_t *>(p);
+    p += (2 * n + 15) & ~15ull;
+    w.slots = reinterpret_cast<uint32_t *>(p);
+    p += (4 * n + 15) & ~15ull;
+    w.packed = reinterpret_cast<U4 *>(p);
+    w.sorted = w.packed + n;
+    return w;
+}
+
+// This workgroup's batch of a key launch (workgroup-uniform).
+__device__ __forceinline__ uint32_t group_chunk_batch(const LocateGroup &grp, uint32_t c) {
+    uint32_t jb = 0;
+#pragma unroll
+    for (uint32_t t = 1; t < kMaxGroup; ++t)
+        if (t < grp.n && c >= grp.chunk_begin[t]) jb = t;
+    return jb;
+}
+
+// 1. Per chunk, NP tiles staged at a time: each pattern's key — its last
+// gkey_len symbols as digits over the symbols that occur in the text, the
+// last symbol most significant (the order in which the backward search reads
+// them) — its symbols packed gbits each (a symbol >= sigma kept as sigma: the
+// search rejects it the same way), and its rank among the chunk's patterns
+// with that key (LDS histogram); then one global add per key reserves the
+// chunk's places among the launch's patterns with that key, and each
+// pattern's place (the chunk's base + its rank) is written.
+template <typename P, int NP>
+__global__ __launch_bounds__(256) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t stage_bytes,
+                                                   uint32_t rec_bytes) {
+    constexpr int R = (int)kGroupChunkTiles;
+    static_assert(R % NP == 0, "whole stagings per chunk");
+    __shared__ Tables<P> s;
+    __shared__ uint32_t hist[kGroupBins];
+    extern __shared__ uint8_t s_pat[];
+    stage_tables(a, s, nullptr);
+    for (uint32_t x = threadIdx.x; x < kGroupBins; x += 256) hist[x] = 0;
+    const uint32_t c = blockIdx.x, jb = group_chunk_batch(grp, c);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t G = (B.npat + 255) / 256, t0 = (uint64_t)(c - grp.chunk_begin[jb]) * R;
+    const bool rev = B.rev != 0;
+    const GroupArrays w = group_arrays(B, rec_bytes);
+    const uint32_t bits = grp.gbits, sym_max = a.sigma;
+    uint32_t key_r[R], rank_r[R];
+#pragma unroll
+    for (int r = 0; r < R; r += NP) {
+        const uint64_t g = t0 + r;
+        if (g < G) {  // (workgroup-uniform)
+            uint64_t beg[NP], end[NP], b0, b1;
+            // (its first barrier also publishes the tables and the zeroed histogram)
+            const bool staged = stage_span<P, NP>(s, s_pat, B.bytes, B.offs, B.npat, g * 256u, rev, stage_bytes,
+                                                  B.stride, a.status, beg, end, b0, b1);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const uint64_t i = (g + q) * 256u + threadIdx.x;
+                key_r[r + q] = 0;
+                rank_r[r + q] = 0;
+                if (i < B.npat) {
+                    const PatView pv = pattern_view(s, s_pat, staged, B.bytes, beg[q], end[q], b0, b1, rev);
+                    uint32_t key = 0;
+                    for (uint32_t k = 0; k < grp.gkey_len; ++k) {
+                        uint32_t d = 0;
+                        if (k < pv.m) {
+                            const uint32_t ck = pv.at(pv.m - 1 - k);
+                            d = ck < (uint32_t)kMaxSigma ? s.dig[ck] : kNoDigit;
+                            d = d == kNoDigit ? 0u : d;  // (such a pattern occurs nowhere)
+                        }
+                        key = key * grp.gkey_base + d;
+                    }
+                    uint64_t lo = 0, hi = 0;  // 128-bit accumulator, 96 bits used
+                    for (uint32_t j = 0; j < (uint32_t)pv.m; ++j) {
+                        uint32_t cj = pv.at(j);
+                        cj = cj < sym_max ? cj : sym_max;
+                        const uint32_t at = j * bits;
+                        if (at < 64) {
+                            lo |= (uint64_t)cj << at;
+                            if (at + bits > 64) hi |= (uint64_t)cj >> (64 - at);
+                        } else {
+                            hi |= (uint64_t)cj << (at - 64);
+                        }
+                    }
+                    key_r[r + q] = key;
+                    rank_r[r + q] = atomicAdd(&hist[key], 1u);
+                    U4 e;
+                    e.x = (uint32_t)lo;
+                    e.y = (uint32_t)(lo >> 32);
+                    e.z = (uint32_t)hi;
+                    e.w = 0u;
+                    w.packed[i] = e;
+                }
+            }
+            __syncthreads();  // (the next staging rewrites s_pat)
+        }
+    }
+    for (uint32_t x = threadIdx.x; x < kGroupBins; x += 256) {
+        const uint32_t h = hist[x];
+        hist[x] = h ? atomicAdd(grp.gcount + x, h) : 0u;  // the chunk's base for key x
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t i = (t0 + r) * 256u + threadIdx.x;
+        if (i < B.npat) {
+            w.keys[i] = (uint16_t)key_r[r];
+            w.slots[i] = hist[key_r[r]] + rank_r[r];
+        }
+    }
+}
+
+// What k_search_grouped needs of each batch, staged in LDS (the batch of a
+// lane's pattern is per lane here, not per workgroup).
+template <typename P>
+struct GroupBatch {
+    SearchRec<P> *recs;
+    const U4 *sorted;
+    uint64_t npat, pend;  // pend: the batches' patterns up to and including this one
+    uint32_t tile_begin, stride;
+};
+
+// 3. Search the launch's patterns in key order: workgroup b takes sorted
+// positions [256 b, 256 b + 256) — their records are read in order, the
+// symbols unpacked into each lane's cap bytes of LDS — searches, walks a single
+// row, and leaves its record at the pattern's own index.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256, 8) void k_search_grouped(const QueryArgs a, const LocateGroup grp,
+                                                           uint64_t total, uint32_t cap, uint32_t xcd) {
+    __shared__ Tables<P> s;
+    __shared__ GroupBatch<P> sb[kMaxGroup];
+    extern __shared__ uint8_t s_pat[];  // 256 x cap B of symbols (cap >= every batch's length), then the k-mer table
+    stage_tables(a, s, s_pat + 256 * cap);
+    if (threadIdx.x == 0) {
+        uint64_t pend = 0;
+        for (uint32_t j = 0; j < grp.n; ++j) {
+            const LocateBatch &B = grp.b[j];
+            const uint64_t G = (B.npat + 255) / 256;
+            pend += B.npat;
+            sb[j].recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
+            sb[j].sorted = group_arrays(B, sizeof(SearchRec<P>)).sorted;
+            sb[j].npat = B.npat;
+            sb[j].pend = pend;
+            sb[j].tile_begin = grp.tile_begin[j];
+            sb[j].stride = B.stride;
+        }
+    }
+    __syncthreads();
+    // xcd: workgroup b takes chunk start(b % 8) + b / 8, so that (under the
+    // round-robin placement of workgroups over the 8 XCDs, which only speed
+    // depends on) each XCD's L2 serves one eighth of the key order
+    uint32_t chunk = blockIdx.x;
+    if (xcd) {
+        const uint32_t q = gridDim.x / 8, rem = gridDim.x % 8, x = blockIdx.x % 8;
+        chunk = x * q + (x < rem ? x : rem) + blockIdx.x / 8;
+    }
+    const uint64_t sp = (uint64_t)chunk * 256u + threadIdx.x;
+    if (sp >= total) return;
+    uint32_t js = 0;
+    for (uint32_t t = 0; t + 1 < grp.n; ++t) js += sp >= sb[t].pend ? 1u : 0u;
+    const U4 e = sb[js].sorted[sp - (sb[js].pend - sb[js].npat)];
+    const uint32_t v = e.w;
+    uint32_t jb = 0;
+    for (uint32_t t = 1; t < grp.n; ++t) jb += (v >> 8) >= sb[t].tile_begin ? 1u : 0u;
+    const GroupBatch<P> &B = sb[jb];
+    const uint64_t i = (uint64_t)(v - B.tile_begin * 256u);
+    const uint32_t m = B.stride, bits = grp.gbits, msk = (1u << bits) - 1u;
+    uint8_t *dst = s_pat + threadIdx.x * cap;
+    const uint64_t lo = (uint64_t)e.x | ((uint64_t)e.y << 32), hi = e.z;
+    for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t at = j * bits;
+        uint64_t x;
+        if (at < 64) {
+            x = lo >> at;
+            if (at + bits > 64) x |= hi << (64 - at);
+        } else {
+            x = hi >> (at - 64);
+        }
+        dst[j] = (uint8_t)(x & msk);
+    }
+    PatView pv;
+    pv.m = m;
+    pv.rev = false;
+    pv.raw = nullptr;
+    pv.enc = s.enc;
+    pv.sym = dst;
+    P lo_r, hi_r, rloc;
+    uint64_t mask;
+    uint32_t mode;
+    const uint32_t bad = search<P, N, VB, REC, kVarFaithful>(a, s, pv, lo_r, hi_r, rloc, mask, mode);
+    if (bad) atomicOr(a.status, bad);
+    if (mode == kHitRows && hi_r - lo_r == P(1)) {
+        rloc = walk_row<P, N, VB, REC>(a, s.C, lo_r);
+        mode = kHitOne;
+    }
+    B.recs[i] = pack_rec<P>(lo_r, hi_r, rloc, mask, mode);
+}
+
 // 3. Output offsets (tile offset + in-tile scan) and every location, rows
 // dealt across each wave's lanes (emit_locations).
 // fold: batches of at most kFoldTiles tiles need no k_scan: each workgroup

@@ -109,6 +109,17 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
     });
 }
 
+[[maybe_unused]] hipError_t op_search_grouped(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
+                                              uint64_t total, uint32_t cap, uint32_t xcd, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        const uint64_t grid = (total + 255) / 256;
+        if (grid == 0 || grid > 0x7FFFFFFFull || cap == 0 || cap > kGroupPackBits) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_search_grouped<P, N, VB, R>), dim3((uint32_t)grid), dim3(256), 256 * cap + qa.kt_lds_bytes,
+                           s, qa, grp, total, cap, xcd);
+        return hipGetLastError();
+    });
+}
+
 [[maybe_unused]] hipError_t op_dlut_level(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
                          void *child, hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
@@ -154,8 +165,8 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 #define FMX_OPS_NAME2(p, n, v) layout_ops_##p##_##n##_##v
 #define FMX_OPS_NAME(p, n, v) FMX_OPS_NAME2(p, n, v)
 extern const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB);
-const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB) = {op_count, op_search, op_emit, op_dlut_level, op_full_sa,
-                                                           op_relayout};
+const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB) = {op_count, op_search, op_emit, op_search_grouped,
+                                                           op_dlut_level, op_full_sa, op_relayout};
 #endif
 
 }  // namespace fmx

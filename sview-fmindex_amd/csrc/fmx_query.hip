@@ -63,6 +63,85 @@ __global__ __launch_bounds__(256) void k_scan(const LocateGroup grp) {
     }
 }
 
+// ---------------------------------------------------------- grouped launches
+// (k_group_key, k_group_place and k_search_grouped: fmx_kernels.hpp)
+
+// 2. The launch's key counts -> each key's first sorted position (exclusive
+// scan in place).
+__global__ __launch_bounds__(256) void k_group_scan(uint32_t *cnt) {
+    __shared__ uint64_t s_scan[4];
+    constexpr uint32_t per = kGroupBins / 256;
+    uint32_t v[per], sum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < per; ++u) {
+        v[u] = cnt[threadIdx.x * per + u];
+        sum += v[u];
+    }
+    uint64_t tot;
+    uint32_t run = (uint32_t)block_excl_scan(sum, &tot, s_scan);
+#pragma unroll
+    for (uint32_t u = 0; u < per; ++u) {
+        cnt[threadIdx.x * per + u] = run;
+        run += v[u];
+    }
+}
+
+// 3. Each pattern's sorted position (its key's first position + its place):
+// there goes its packed record, tagged with its pattern id (tile_begin * 256
+// + index).  The sorted order is held by the batches one after another.
+__global__ __launch_bounds__(256) void k_group_place(const LocateGroup grp, uint32_t rec_bytes) {
+    __shared__ U4 *s_sorted[kMaxGroup];
+    __shared__ uint64_t s_pend[kMaxGroup];
+    if (threadIdx.x == 0) {
+        uint64_t pend = 0;
+        for (uint32_t j = 0; j < grp.n; ++j) {
+            pend += grp.b[j].npat;
+            s_sorted[j] = group_arrays(grp.b[j], rec_bytes).sorted;
+            s_pend[j] = pend;
+        }
+    }
+    __syncthreads();
+    const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t i = (uint64_t)(vt - grp.tile_begin[jb]) * 256u + threadIdx.x;
+    if (i >= B.npat) return;
+    const GroupArrays w = group_arrays(B, rec_bytes);
+    const uint64_t sp = (uint64_t)grp.gcount[w.keys[i]] + w.slots[i];
+    uint32_t js = 0;
+    for (uint32_t t = 0; t + 1 < grp.n; ++t) js += sp >= s_pend[t] ? 1u : 0u;
+    const uint64_t first = js ? s_pend[js - 1] : 0;
+    U4 e = w.packed[i];
+    e.w = vt * 256u + threadIdx.x;
+    s_sorted[js][sp - first] = e;
+}
+
+// 4. Each tile's count (k_emit's tile offsets) and each pattern's count (the
+// optional counts output, in order here), and the key counters zeroed again
+// for the workspace's next grouped launch.
+template <typename P>
+__global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp, uint32_t tiles) {
+    __shared__ uint64_t s_w[4];
+    const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t G = (B.npat + 255) / 256, g = vt - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
+    const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
+    uint64_t cnt = 0;
+    if (i < B.npat) {
+        P lo, rloc;
+        uint64_t mask;
+        uint32_t mode;
+        cnt = unpack_rec<P>(recs[i], lo, rloc, mask, mode);
+        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = (P)cnt;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = cnt;
+    for (uint64_t x = (uint64_t)vt * 256u + threadIdx.x; x < kGroupBins; x += (uint64_t)tiles * 256u)
+        grp.gcount[x] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) B.tiles[g] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
 // ------------------------------------------------------------ deep k-mer table
 
 // The table's digits are the S symbols that occur in the text (dlut_sym).
@@ -196,11 +275,74 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
     return d.ops->count(qa, d.vb, d.rec, search_var(qa, sb), d_bytes, d_offsets, n, flags, d_counts, sb, stream);
 }
 
+// A grouped launch's search (kWsHeader): keys and chunk bases, sorted order,
+// search in key order, counts.
+static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
+                                        uint64_t total, uint32_t sb, uint32_t bits, hipStream_t stream) {
+    const Disp d = dispatch(ix);
+    grp.gcount = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader + 256);
+    grp.gkey_len = ix->gkey_len;
+    grp.gkey_base = ix->gkey_base;
+    grp.gbits = bits;
+    uint32_t chunks = 0;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        grp.chunk_begin[j] = chunks;
+        chunks += (uint32_t)group_chunks(grp.b[j].npat);
+    }
+    const bool p4 = ix->bv.L.pos_bytes == 4;
+    const uint32_t rb = (uint32_t)locate_rec_bytes(ix->bv.L.pos_bytes);
+    // the key kernel stages four tiles at a time when their bytes fit 32 KB of LDS
+    uint32_t maxm = 1;
+    for (uint32_t j = 0; j < grp.n; ++j) maxm = std::max<uint32_t>(maxm, grp.b[j].stride);
+    const bool four = 4u * 256u * maxm + 16 <= 32768u;
+    const uint32_t ksb = four ? 32768u : std::max<uint32_t>(sb, 256u * maxm + 16);
+    if (p4 && four)
+        hipLaunchKernelGGL((k_group_key<uint32_t, 4>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
+    else if (p4)
+        hipLaunchKernelGGL((k_group_key<uint32_t, 1>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
+    else if (four)
+        hipLaunchKernelGGL((k_group_key<uint64_t, 4>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
+    else
+        hipLaunchKernelGGL((k_group_key<uint64_t, 1>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);
+    hipLaunchKernelGGL(k_group_place, dim3(tiles), dim3(256), 0, stream, grp, rb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // each lane unpacks its pattern into `cap` bytes of LDS: the longest batch's length, 4-byte aligned
+    uint32_t cap = 4;
+    for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
+    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_xcd, stream)) != hipSuccess)
+        return e;
+    if (p4)
+        hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(tiles), dim3(256), 0, stream, grp, tiles);
+    else
+        hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(tiles), dim3(256), 0, stream, grp, tiles);
+    return hipGetLastError();
+}
+
+// Bits per packed symbol for a grouped launch of `grp`, or 0 when it cannot
+// be grouped: every batch fixed-length with its patterns within kGroupPackBits.
+static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup &grp) {
+    uint32_t bits = 1;
+    while ((1u << bits) < ix->bv.sigma + 1) ++bits;
+    for (uint32_t j = 0; j < grp.n; ++j)
+        if (grp.b[j].stride == 0 || grp.b[j].stride * bits > kGroupPackBits) return 0;
+    return bits;
+}
+
 // The kernels of a (grouped) locate, one after another on `stream`.
-static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp, uint32_t tiles,
+static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp_in, uint32_t tiles,
                                uint32_t sb, hipStream_t stream, hipEvent_t mid = nullptr) {
     const Disp d = dispatch(ix);
-    hipError_t e = d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
+    LocateGroup grp = grp_in;
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < grp.n; ++j) total += grp.b[j].npat;
+    const uint32_t bits = group_pack_bits(ix, grp);
+    const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= ix->grouped_min && !grp.tile_ctr &&
+                         search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
+    hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, tiles, total, sb, bits, stream)
+                           : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     uint32_t fold = 1;

@@ -183,7 +183,9 @@ class ShardedLocate:
     runs the shard (FmIndex by default: fmx_locate_batch_async on `stream`,
     else on the caller's current stream — the stream the shard's inputs and
     output buffers were made on, so the launch is ordered after them; a
-    given stream first waits for the current one); if the shard has more
+    given stream, or the stream of its own that stands in for torch's null
+    default stream (null means the index's own stream to the ABI), first
+    waits for the current one); if the shard has more
     occurrences than the first guess of room, it runs again with exactly
     enough.  Host round trips per call: the shard's byte range, its location
     total and the size exchange."""
@@ -199,6 +201,7 @@ class ShardedLocate:
         self.dtype = dtype or (torch.int32 if ix is None or ix.position.nbytes == 4 else torch.int64)
         self.locate_fn = locate_fn or self._index_locate
         self._ws = None
+        self._own = None
         self.last = {}
 
     def _index_locate(self, d_bytes, d_offsets, m, counts, locs, cap):
@@ -209,9 +212,17 @@ class ShardedLocate:
         loff = torch.zeros(m + 1, dtype=torch.int64, device=d_offsets.device)
         need = torch.zeros(1, dtype=torch.int64, device=d_offsets.device)
         cur = torch.cuda.current_stream(d_offsets.device)
-        if self.stream is not None:  # ordered after everything the current stream made
-            self.stream.wait_stream(cur)
-        st = (self.stream or cur).cuda_stream
+        run_on = self.stream
+        if run_on is None and cur.cuda_stream == 0:
+            # torch's default stream is the null stream, and a null stream
+            # means the index's own (unordered) stream to the ABI: run on a
+            # stream of ours that waits for it instead
+            if self._own is None:
+                self._own = torch.cuda.Stream(device=d_offsets.device)
+            run_on = self._own
+        if run_on is not None:  # ordered after everything the current stream made
+            run_on.wait_stream(cur)
+        st = (run_on or cur).cuda_stream
         self.ix.locate_batch_async(d_bytes.data_ptr() if d_bytes.numel() else 0, d_offsets.data_ptr(), m,
                                    loff.data_ptr(), locs.data_ptr() if cap else 0, cap, need.data_ptr(),
                                    self._ws.data_ptr(), self._ws.numel(), d_counts=counts.data_ptr() if m else 0,
