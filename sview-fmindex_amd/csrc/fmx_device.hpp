@@ -5,6 +5,10 @@
 // __host__ __device__ so the CPU suite runs exactly the code the GPU runs.
 #pragma once
 
+#ifndef FMX_NT_NARROW
+#define FMX_NT_NARROW 0  // A/B builds: -DFMX_NT_NARROW=1 (see Occ::hot_fetch)
+#endif
+
 #include "fmx_internal.hpp"
 
 #define FMX_HD __host__ __device__ __forceinline__
@@ -244,11 +248,23 @@ struct Occ {
     // C2: 64-B records of 64 rows) lie below 2^32 bytes for every position
     // (q * RB <= p & ~(VB - 1) < 2^32): a 32-bit offset from the records' base.
     static constexpr bool OFF32 = sizeof(P) == 4 && RB == VB;
+    // NT: a record read by one pattern only (a narrow interval's step, a walk
+    // step) is loaded non-temporally where FMX_NT_NARROW is built in (A/B),
+    // so that it does not displace the records wide intervals share
+    template <bool NT = false>
     FMX_HD static Hot hot_fetch(const QueryArgs &a, uint64_t q, uint32_t c) {
         const uint8_t *u;
         if constexpr (OFF32) u = a.occ + ((uint32_t)q * (uint32_t)RB + c * (uint32_t)U);
         else if constexpr (MULTI) u = a.occ + q * RB + (c / (uint32_t)PL) * 128u + (c % (uint32_t)PL) * (uint32_t)U;
         else u = a.occ + q * RB + c * U;
+#if defined(__HIP_DEVICE_COMPILE__) && FMX_NT_NARROW
+        if constexpr (NT) {
+            uint32_t d[U / 4];
+#pragma unroll
+            for (int j = 0; j < U / 4; ++j) d[j] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(u) + j);
+            return hot_from(d);
+        }
+#endif
         return hot_from(reinterpret_cast<const Unit *>(u)->d);  // one U-byte load
     }
     // Occ(c, block start + rem): the stored checkpoint and the mask's first rem
@@ -324,9 +340,20 @@ struct Occ {
     FMX_HD static void rank_pair(const QueryArgs &a, P plo, P phi, uint32_t c, P &rlo, P &rhi) {
         const uint64_t ql = (uint64_t)plo / VB, qh = (uint64_t)phi / VB;
         if constexpr (ONEHOT) {
+#if FMX_NT_NARROW
+            Hot hl, hh;
+            if (qh == ql) {
+                hl = hot_fetch<true>(a, ql, c);
+                hh = hl;
+            } else {
+                hl = hot_fetch(a, ql, c);
+                hh = hot_fetch(a, qh, c);
+            }
+#else
             const Hot hl = hot_fetch(a, ql, c);
             Hot hh = hl;
             if (qh != ql) hh = hot_fetch(a, qh, c);
+#endif
             rlo = hot_occ(hl, (uint32_t)((uint64_t)plo % VB));
             rhi = hot_occ(hh, (uint32_t)((uint64_t)phi % VB));
             return;
@@ -370,7 +397,13 @@ struct Occ {
             const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
             V4 ch[NCH];
 #pragma unroll
-            for (int i = 0; i < NCH; ++i) ch[i] = rp[i];
+            for (int i = 0; i < NCH; ++i) {
+#if defined(__HIP_DEVICE_COMPILE__) && FMX_NT_NARROW
+                ch[i] = __builtin_nontemporal_load(rp + i);
+#else
+                ch[i] = rp[i];
+#endif
+            }
             Hot hs[NCK2];
             c = 0;
 #pragma unroll
