@@ -416,93 +416,110 @@ __device__ __forceinline__ uint32_t group_chunk_batch(const LocateGroup &grp, ui
     return jb;
 }
 
-// 1. Per chunk, NP tiles staged at a time: each pattern's key — its last
-// gkey_len symbols as digits over the symbols that occur in the text, the
-// last symbol most significant (the order in which the backward search reads
-// them) — its symbols packed gbits each (a symbol >= sigma kept as sigma: the
-// search rejects it the same way), and its rank among the chunk's patterns
-// with that key (LDS histogram); then one global add per key reserves the
-// chunk's places among the launch's patterns with that key, and each
-// pattern's place (the chunk's base + its rank) is written.
-template <typename P, int NP>
-__global__ __launch_bounds__(256) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t stage_bytes,
-                                                   uint32_t rec_bytes) {
-    constexpr int R = (int)kGroupChunkTiles;
-    static_assert(R % NP == 0, "whole stagings per chunk");
-    __shared__ Tables<P> s;
+// 1. Per chunk of kGroupChunkTiles tiles (1,024 threads, two patterns each,
+// fixed length m <= 4 W - 3 bytes): each pattern's bytes as W aligned words
+// straight into registers (consecutive patterns lie back to back, so a wave's
+// loads are contiguous); its key — its last gkey_len symbols as digits over
+// the symbols that occur in the text, the last symbol most significant (the
+// order in which the backward search reads them) — and its symbols packed
+// gbits each (a symbol >= sigma kept as sigma: the search rejects it the same
+// way), decoded byte by byte with compile-time register indices; its rank
+// among the chunk's patterns with that key (LDS histogram); then one global
+// add per key reserves the chunk's places among the launch's patterns with
+// that key, and each pattern's place (the chunk's base + its rank) is
+// written.  The offsets are checked against the length hint here (the
+// grouped search never reads them).
+template <int W>
+__global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
+    constexpr uint32_t T = 1024, PPT = kGroupChunkTiles * 256 / T;  // patterns per thread
+    __shared__ uint8_t s_enc[256];
+    __shared__ uint8_t s_dig[kMaxSigma];
+    __shared__ uint32_t s_pw[32];
     __shared__ uint32_t hist[kGroupBins];
-    extern __shared__ uint8_t s_pat[];
-    stage_tables(a, s, nullptr);
-    for (uint32_t x = threadIdx.x; x < kGroupBins; x += 256) hist[x] = 0;
-    const uint32_t c = blockIdx.x, jb = group_chunk_batch(grp, c);
-    const LocateBatch &B = grp.b[jb];
-    const uint64_t G = (B.npat + 255) / 256, t0 = (uint64_t)(c - grp.chunk_begin[jb]) * R;
-    const bool rev = B.rev != 0;
-    const GroupArrays w = group_arrays(B, rec_bytes);
-    const uint32_t bits = grp.gbits, sym_max = a.sigma;
-    uint32_t key_r[R], rank_r[R];
-#pragma unroll
-    for (int r = 0; r < R; r += NP) {
-        const uint64_t g = t0 + r;
-        if (g < G) {  // (workgroup-uniform)
-            uint64_t beg[NP], end[NP], b0, b1;
-            // (its first barrier also publishes the tables and the zeroed histogram)
-            const bool staged = stage_span<P, NP>(s, s_pat, B.bytes, B.offs, B.npat, g * 256u, rev, stage_bytes,
-                                                  B.stride, a.status, beg, end, b0, b1);
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                const uint64_t i = (g + q) * 256u + threadIdx.x;
-                key_r[r + q] = 0;
-                rank_r[r + q] = 0;
-                if (i < B.npat) {
-                    const PatView pv = pattern_view(s, s_pat, staged, B.bytes, beg[q], end[q], b0, b1, rev);
-                    uint32_t key = 0;
-                    for (uint32_t k = 0; k < grp.gkey_len; ++k) {
-                        uint32_t d = 0;
-                        if (k < pv.m) {
-                            const uint32_t ck = pv.at(pv.m - 1 - k);
-                            d = ck < (uint32_t)kMaxSigma ? s.dig[ck] : kNoDigit;
-                            d = d == kNoDigit ? 0u : d;  // (such a pattern occurs nowhere)
-                        }
-                        key = key * grp.gkey_base + d;
-                    }
-                    uint64_t lo = 0, hi = 0;  // 128-bit accumulator, 96 bits used
-                    for (uint32_t j = 0; j < (uint32_t)pv.m; ++j) {
-                        uint32_t cj = pv.at(j);
-                        cj = cj < sym_max ? cj : sym_max;
-                        const uint32_t at = j * bits;
-                        if (at < 64) {
-                            lo |= (uint64_t)cj << at;
-                            if (at + bits > 64) hi |= (uint64_t)cj >> (64 - at);
-                        } else {
-                            hi |= (uint64_t)cj << (at - 64);
-                        }
-                    }
-                    key_r[r + q] = key;
-                    rank_r[r + q] = atomicAdd(&hist[key], 1u);
-                    U4 e;
-                    e.x = (uint32_t)lo;
-                    e.y = (uint32_t)(lo >> 32);
-                    e.z = (uint32_t)hi;
-                    e.w = 0u;
-                    w.packed[i] = e;
-                }
-            }
-            __syncthreads();  // (the next staging rewrites s_pat)
+    const uint32_t t = threadIdx.x;
+    if (t < 256) s_enc[t] = a.enc[t];
+    if (t < (uint32_t)kMaxSigma) s_dig[t] = a.dlut_dig[t] == kNoDigit ? 0 : a.dlut_dig[t];  // (absent: occurs nowhere)
+    if (t == 0) {
+        uint32_t w = 1;
+        for (uint32_t e = 0; e < 32; ++e) {
+            s_pw[e] = w;  // base^e while it fits the key
+            w = e + 1 < grp.gkey_len ? w * grp.gkey_base : w;
         }
     }
-    for (uint32_t x = threadIdx.x; x < kGroupBins; x += 256) {
-        const uint32_t h = hist[x];
-        hist[x] = h ? atomicAdd(grp.gcount + x, h) : 0u;  // the chunk's base for key x
+    for (uint32_t x = t; x < kGroupBins; x += T) hist[x] = 0;
+    __syncthreads();
+    const uint32_t c = blockIdx.x, jb = group_chunk_batch(grp, c);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t n = B.npat, first = (uint64_t)(c - grp.chunk_begin[jb]) * kGroupChunkTiles * 256u;
+    const uint32_t m = B.stride, bits = grp.gbits, sym_max = a.sigma, L = grp.gkey_len;
+    const bool rev = B.rev != 0;
+    const GroupArrays w = group_arrays(B, rec_bytes);
+    if (first == 0 && t == 0 && B.offs[0] != 0) atomicOr(a.status, kStatusStride);
+    uint32_t x[PPT][W], lead[PPT];
+    uint64_t chk[PPT];
+#pragma unroll
+    for (uint32_t p = 0; p < PPT; ++p) {
+        const uint64_t i = first + p * T + t;
+        const uint64_t beg = i * m, a0 = beg & ~3ull;
+        lead[p] = (uint32_t)(beg - a0);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(B.bytes + a0);
+        const bool ok = i < n;
+#pragma unroll
+        for (uint32_t q = 0; q < W; ++q) x[p][q] = ok && 4 * q < lead[p] + m ? src[q] : 0u;
+        chk[p] = ok ? B.offs[i + 1] : 0;
+    }
+    uint32_t key_r[PPT], rank_r[PPT];
+#pragma unroll
+    for (uint32_t p = 0; p < PPT; ++p) {
+        const uint64_t i = first + p * T + t;
+        key_r[p] = rank_r[p] = 0;
+        if (i >= n) continue;
+        if (chk[p] != (i + 1) * m) atomicOr(a.status, kStatusStride);
+        uint64_t lo = 0, hi = 0;
+        uint32_t key = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4 * W; ++b) {
+            const uint32_t pos = b - lead[p];  // input byte index (wraps below 0: skipped)
+            if (pos >= m) continue;
+            const uint32_t j = rev ? m - 1 - pos : pos;  // pattern position
+            uint32_t cj = s_enc[(x[p][b >> 2] >> (8 * (b & 3))) & 0xffu];
+            const uint32_t back = m - 1 - j;  // 0 = the last symbol
+            if (back < L) key += (cj < (uint32_t)kMaxSigma ? s_dig[cj] : 0u) * s_pw[L - 1 - back];
+            cj = cj < sym_max ? cj : sym_max;
+            const uint32_t at = j * bits;
+            if (at < 64) {
+                lo |= (uint64_t)cj << at;
+                if (at + bits > 64) hi |= (uint64_t)cj >> (64 - at);
+            } else {
+                hi |= (uint64_t)cj << (at - 64);
+            }
+        }
+        key_r[p] = key;
+        rank_r[p] = atomicAdd(&hist[key], 1u);
+        U4 e;
+        e.x = (uint32_t)lo;
+        e.y = (uint32_t)(lo >> 32);
+        e.z = (uint32_t)hi;
+        e.w = 0u;
+        w.packed[i] = e;
     }
     __syncthreads();
+    // every add of a thread in flight at once
+    constexpr uint32_t per = kGroupBins / T;
+    uint32_t h[per], base[per];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint64_t i = (t0 + r) * 256u + threadIdx.x;
-        if (i < B.npat) {
-            w.keys[i] = (uint16_t)key_r[r];
-            w.slots[i] = hist[key_r[r]] + rank_r[r];
+    for (uint32_t u = 0; u < per; ++u) h[u] = hist[u * T + t];
+#pragma unroll
+    for (uint32_t u = 0; u < per; ++u) base[u] = h[u] ? atomicAdd(grp.gcount + u * T + t, h[u]) : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < per; ++u) hist[u * T + t] = base[u];  // the chunk's base for each key
+    __syncthreads();
+#pragma unroll
+    for (uint32_t p = 0; p < PPT; ++p) {
+        const uint64_t i = first + p * T + t;
+        if (i < n) {
+            w.keys[i] = (uint16_t)key_r[p];
+            w.slots[i] = hist[key_r[p]] + rank_r[p];
         }
     }
 }

@@ -291,19 +291,13 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     }
     const bool p4 = ix->bv.L.pos_bytes == 4;
     const uint32_t rb = (uint32_t)locate_rec_bytes(ix->bv.L.pos_bytes);
-    // the key kernel stages four tiles at a time when their bytes fit 32 KB of LDS
+    // the key kernel holds each pattern in W registers: 8 words up to 29 bytes, else 25 (96 bytes)
     uint32_t maxm = 1;
     for (uint32_t j = 0; j < grp.n; ++j) maxm = std::max<uint32_t>(maxm, grp.b[j].stride);
-    const bool four = 4u * 256u * maxm + 16 <= 32768u;
-    const uint32_t ksb = four ? 32768u : std::max<uint32_t>(sb, 256u * maxm + 16);
-    if (p4 && four)
-        hipLaunchKernelGGL((k_group_key<uint32_t, 4>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
-    else if (p4)
-        hipLaunchKernelGGL((k_group_key<uint32_t, 1>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
-    else if (four)
-        hipLaunchKernelGGL((k_group_key<uint64_t, 4>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
+    if (maxm <= 29)
+        hipLaunchKernelGGL(k_group_key<8>, dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     else
-        hipLaunchKernelGGL((k_group_key<uint64_t, 1>), dim3(chunks), dim3(256), ksb, stream, qa, grp, ksb, rb);
+        hipLaunchKernelGGL(k_group_key<25>, dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);
