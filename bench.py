@@ -82,13 +82,15 @@ CONFIGS = {
     "c1": dict(text_len=1_000_000, alphabet=b"ACGT", symbols=[b"Aa", b"Cc", b"Gg", b"Tt"], pos=4, planes=2,
                vec=64, k=3, sr=2, patterns=1_000, m=20, total=0, group=16, streams=8,
                desc="C1: 1 Mbp ACGT, 1,000 x 20 bp, u32/Block2<u64>, sr 2, k 3"),
-    # configs[1]: the headline (metric quoted on it)
+    # configs[1]: the headline (metric quoted on it).  16 batches per launch: a grouped launch of
+    # 1.6 M patterns shares more of its first LF steps than one of 0.8 M (2.72 vs 2.59e9 grouped,
+    # 2.59 vs 2.55e9 in launch order; profiles/r3/grouped/r3g6)
     "c2": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
-               patterns=100_000, m=20, total=0,
+               patterns=100_000, m=20, total=0, group=16,
                desc="C2: 1 Gbp ACGT (ACGTN, N wildcard), 100,000 x 20 bp per GPU, u32/Block3<u64>, sr 2, k 3"),
     # configs[2]: 10 M patterns sharded over the GPUs
     "c3": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
-               patterns=100_000, m=20, total=10_000_000,
+               patterns=100_000, m=20, total=10_000_000, group=16,
                desc="C3: 1 Gbp ACGT, 10,000,000 x 20 bp sharded over the GPUs, u32/Block3<u64>, sr 2, k 3"),
     # configs[3]: large-alphabet occ path
     "c4": dict(text_len=1_000_000_000, alphabet=AMINO, symbols=[bytes([c, c + 32]) for c in AMINO] + [b"Xx"],
@@ -140,7 +142,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
     ap.add_argument("--batches", type=int, default=32, help="distinct batches cycled (weak-scaling configs)")
-    ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 16; default 8, c1: 16)")
+    ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 16; default 8; c1, c2, c3: 16)")
     ap.add_argument("--graph", action="store_true",
                     help="capture one pass (every launch, forked over the streams) in a HIP graph and replay it: "
                          "one host call per pass instead of one per launch (launch-bound configs)")
@@ -755,6 +757,8 @@ def main():
     search_us = ks["total_ms"] / ks["launches"] * 1e3 if ks.get("launches") else float("nan")
     k_achieved = alg_per_pattern * ppl / (search_us * 1e-6) / 1e9
     key = f"{args.config}:{n}:{B}:{m}:{info['options']}:g{GR}"
+    grouped = bool(info.get("group_key_len")) and B * GR >= info["grouped_min"] and bool(fixed) and \
+        m * table.symbol_count().bit_length() <= 96
     tr = traffic_of(args.traffic_json, key)
     roof = {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -763,13 +767,16 @@ def main():
                           "alg_bytes_per_pattern) x the timed region's patterns/s per GPU",
         "alg_bytes_per_pattern": alg_per_pattern,
         "kernel": {
-            "name": "k_search", "avg_us": search_us, "patterns_per_launch": ppl,
+            "name": ("search phase of a grouped launch: k_group_key + k_group_scan + k_group_place + "
+                     "k_search_grouped + k_group_tiles" if grouped else "k_search"),
+            "avg_us": search_us, "patterns_per_launch": ppl,
             "achieved": k_achieved, "frac": k_achieved / HBM_PEAK_GBS,
             "emit_avg_us": ke["total_ms"] / ke["launches"] * 1e3 if ke.get("launches") else None,
             "launch_avg_us": kl["total_ms"] / kl["launches"] * 1e3 if kl.get("launches") else None,
             "launches": ks.get("launches", 0),
-            "basis": "alg bytes x patterns per launch / k_search's average duration: launches one after another "
-                     "on one stream, nothing else in flight, HIP events around k_search alone (compare "
+            "basis": "alg bytes x patterns per launch / the search phase's average duration: launches one after "
+                     "another on one stream, nothing else in flight, HIP events around the search phase (k_search, "
+                     "or a grouped launch's five kernels before k_emit) alone (compare the sum of those kernels in "
                      "rocprofv3 --kernel-trace --stats of bench.py --streams 1)",
         },
     }
@@ -825,9 +832,7 @@ def main():
             "parallelism": f"dp{world} (patterns sharded, blob replicated)",
             "streams": S, "fixed_len_hint": fixed, "batches_per_launch": GR, "distinct_batches": len(w.batches),
             "hip_graph": bool(args.graph),
-            "launch_order": (f"grouped by the last {info['group_key_len']} symbols"
-                             if info.get("group_key_len") and B * GR >= info["grouped_min"] and fixed
-                             and m * (table.symbol_count()).bit_length() <= 96 else "as given"),
+            "launch_order": f"grouped by the last {info['group_key_len']} symbols" if grouped else "as given",
         },
         "roofline": roof,
         "kernels_ms_per_launch_timed_region": per_launch_ms(timing),

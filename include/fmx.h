@@ -141,8 +141,7 @@ typedef struct fmx_index_info {
     uint32_t group_key_len;  /* grouped launches: the key's last symbols (0: none) */
     uint32_t group_key_base; /* ... as digits over this many symbols               */
     uint64_t grouped_min;    /* fixed-length launches of at least this many
-                                patterns are grouped (UINT64_MAX: never, the
-                                default)                                            */
+                                patterns are grouped (UINT64_MAX: never)            */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {
@@ -232,14 +231,14 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
  * workspace is zeroed by the caller before its first use, then belongs to
  * this index: its launches are ordered on one stream at a time (every launch
  * leaves the key counters zero again).  A locate is k_search + k_emit.  A
- * grouped locate (opt-in, environment at load: FMX_GROUPED=1, or
- * FMX_GROUPED_MIN=<patterns per launch>; fixed-length batches whose
- * patterns pack into 96 bits, faithful index) first deals its patterns out
- * in the order of their last symbols, so that patterns whose backward
- * searches share their first LF steps run side by side, and searches them in
- * that order — same results; measured slower than launch order on MI355X
- * (DESIGN.md §5), hence off by default.  No kernel makes one workgroup wait
- * on another. */
+ * grouped locate first deals the launch's patterns out in the order of their
+ * last symbols, so that patterns whose backward searches share their first
+ * LF steps run side by side, and searches them in that order — same
+ * results.  Grouped by default: launches (a group call's batches together) of
+ * at least 131,072 fixed-length patterns that pack into 96 bits, on the
+ * faithful index, when the key spans at least 5 symbols (DNA: 6; environment
+ * at load: FMX_GROUPED=0 never, =1 always, FMX_GROUPED_MIN=<patterns>).  No
+ * kernel makes one workgroup wait on another. */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)

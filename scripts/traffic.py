@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LAUNCH = ("k_search", "k_emit", "k_scan")
+LAUNCH = ("k_search", "k_emit", "k_scan", "k_group_")  # k_group_*: a grouped launch's other kernels
 
 
 def sums(path, variant):
@@ -29,7 +29,9 @@ def sums(path, variant):
         name = r["Kernel_Name"]
         if not any(k in name for k in LAUNCH):
             continue
-        if "k_search" in name:
+        if "k_search_grouped" in name:  # (faithful only)
+            launches.add(r["Dispatch_Id"])
+        elif "k_search" in name:
             if variant not in name:
                 continue
             launches.add(r["Dispatch_Id"])

@@ -467,13 +467,16 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     ix->gkey_len = 0;
     if (S >= 2)
         for (uint64_t bins = S; bins <= kGroupBins && ix->gkey_len < 16; bins *= S) ++ix->gkey_len;
-    // off by default: measured slower on every config ("Grouped launches")
-    ix->grouped_min = ~0ull;
+    // on by default for launches of at least 131,072 patterns whose key spans
+    // at least 5 symbols (DNA: 6; a 20-residue alphabet keys on 2 only and
+    // shares too little): DESIGN.md §5, "Grouped launches"
+    ix->grouped_min = ix->gkey_len >= 5 ? 131072 : ~0ull;
     if (const char *e = getenv("FMX_GROUPED")) {
         if (e[0] == '0') ix->grouped_min = ~0ull;
         else if (e[0] == '1') ix->grouped_min = 1;
     }
     if (const char *e = getenv("FMX_GROUPED_MIN")) ix->grouped_min = strtoull(e, nullptr, 10);
+    ix->grouped_xcd = 1;
     if (const char *e = getenv("FMX_GROUPED_XCD")) ix->grouped_xcd = e[0] == '1';
     if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
         // the largest K with S^K * 2P <= budget, deeper than the blob's k;

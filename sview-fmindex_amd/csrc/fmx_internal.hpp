@@ -245,7 +245,7 @@ constexpr uint64_t kFoldTiles = 2048;
 // finds them zero whatever its n.
 constexpr uint32_t kGroupKeyBits = 12;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
-constexpr uint32_t kGroupChunkTiles = 8;    // tiles (of 256 patterns) per key workgroup
+constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key workgroup
 constexpr uint32_t kGroupPackBits = 96;
 constexpr uint32_t kGroupCounterRoom = kGroupBins;
 constexpr uint64_t kWsHeader = 256 + 4ull * kGroupCounterRoom;

@@ -416,7 +416,7 @@ __device__ __forceinline__ uint32_t group_chunk_batch(const LocateGroup &grp, ui
     return jb;
 }
 
-// 1. Per chunk of kGroupChunkTiles tiles (1,024 threads, two patterns each,
+// 1. Per chunk of kGroupChunkTiles tiles (1,024 threads, four patterns each,
 // fixed length m <= 4 W - 3 bytes): each pattern's bytes as W aligned words
 // straight into registers (consecutive patterns lie back to back, so a wave's
 // loads are contiguous); its key — its last gkey_len symbols as digits over
@@ -455,34 +455,39 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
     const bool rev = B.rev != 0;
     const GroupArrays w = group_arrays(B, rec_bytes);
     if (first == 0 && t == 0 && B.offs[0] != 0) atomicOr(a.status, kStatusStride);
-    uint32_t x[PPT][W], lead[PPT];
-    uint64_t chk[PPT];
+    // G patterns' words in flight at once (all of a thread's when they are short)
+    constexpr uint32_t G = W <= 8 ? PPT : 1;
+    uint32_t key_r[PPT], rank_r[PPT];
 #pragma unroll
-    for (uint32_t p = 0; p < PPT; ++p) {
-        const uint64_t i = first + p * T + t;
+    for (uint32_t p0 = 0; p0 < PPT; p0 += G) {
+    uint32_t x[G][W], lead[G];
+    uint64_t chk[G];
+#pragma unroll
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint64_t i = first + (p0 + g) * T + t;
         const uint64_t beg = i * m, a0 = beg & ~3ull;
-        lead[p] = (uint32_t)(beg - a0);
+        lead[g] = (uint32_t)(beg - a0);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(B.bytes + a0);
         const bool ok = i < n;
 #pragma unroll
-        for (uint32_t q = 0; q < W; ++q) x[p][q] = ok && 4 * q < lead[p] + m ? src[q] : 0u;
-        chk[p] = ok ? B.offs[i + 1] : 0;
+        for (uint32_t q = 0; q < W; ++q) x[g][q] = ok && 4 * q < lead[g] + m ? src[q] : 0u;
+        chk[g] = ok ? B.offs[i + 1] : 0;
     }
-    uint32_t key_r[PPT], rank_r[PPT];
 #pragma unroll
-    for (uint32_t p = 0; p < PPT; ++p) {
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t p = p0 + g;
         const uint64_t i = first + p * T + t;
         key_r[p] = rank_r[p] = 0;
         if (i >= n) continue;
-        if (chk[p] != (i + 1) * m) atomicOr(a.status, kStatusStride);
+        if (chk[g] != (i + 1) * m) atomicOr(a.status, kStatusStride);
         uint64_t lo = 0, hi = 0;
         uint32_t key = 0;
 #pragma unroll
         for (uint32_t b = 0; b < 4 * W; ++b) {
-            const uint32_t pos = b - lead[p];  // input byte index (wraps below 0: skipped)
+            const uint32_t pos = b - lead[g];  // input byte index (wraps below 0: skipped)
             if (pos >= m) continue;
             const uint32_t j = rev ? m - 1 - pos : pos;  // pattern position
-            uint32_t cj = s_enc[(x[p][b >> 2] >> (8 * (b & 3))) & 0xffu];
+            uint32_t cj = s_enc[(x[g][b >> 2] >> (8 * (b & 3))) & 0xffu];
             const uint32_t back = m - 1 - j;  // 0 = the last symbol
             if (back < L) key += (cj < (uint32_t)kMaxSigma ? s_dig[cj] : 0u) * s_pw[L - 1 - back];
             cj = cj < sym_max ? cj : sym_max;
@@ -502,6 +507,7 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
         e.z = (uint32_t)hi;
         e.w = 0u;
         w.packed[i] = e;
+    }
     }
     __syncthreads();
     // every add of a thread in flight at once

@@ -1,8 +1,9 @@
 """Grouped launches (fmx_internal.hpp kWsHeader): a launch's
 patterns searched in the order of their last symbols instead of the order
-given (opt-in).  A launch is grouped when its batches are fixed-length with
-patterns that pack into 96 bits; FMX_GROUPED=1 groups every such launch,
-however small, so the parity tests below run the key / sorted-order / grouped-search
+given.  A launch is grouped when its batches are fixed-length with
+patterns that pack into 96 bits (by default from 131,072 patterns, with a key
+of at least 5 symbols); FMX_GROUPED=1 groups every such launch, however
+small, so the parity tests below run the key / sorted-order / grouped-search
 / count kernels on fixed-length batches of every layout and alphabet size,
 forward and reversed, with absent, wildcard and out-of-alphabet symbols,
 several batches per launch and many launches on one workspace — each result
@@ -124,10 +125,10 @@ def test_out_of_alphabet_grouped(pkg, O, grouped):
 
 
 def test_grouped_equals_launch_order(pkg, O, monkeypatch):
-    """A 300k-pattern fixed-length launch on a 4 Mbp text grouped
-    (FMX_GROUPED_MIN below its size) answers exactly like the same launch in
-    launch order (the default), and like the oracle; the index reports the
-    grouping it applies."""
+    """A 300k-pattern fixed-length launch on a 4 Mbp text grouped (the
+    default above 131,072 patterns; FMX_GROUPED_MIN moves the threshold)
+    answers exactly like the same launch in launch order (FMX_GROUPED=0), and
+    like the oracle; the index reports the grouping it applies."""
     rng = np.random.default_rng(5)
     chars = b"ACGT"
     text = rand_text(rng, chars, 4_000_000, 4_000_000)
@@ -137,8 +138,14 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
     data, offsets = pkg.pack_patterns(pats)
     res = {}
     monkeypatch.delenv("FMX_GROUPED", raising=False)
+    monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    assert ix.info()["grouped_min"] == 131072  # the default for a key of at least 5 symbols
+    ix.close()
+    monkeypatch.setenv("FMX_GROUPED", "0")
     for mode in ("0", None):
         if mode is None:
+            monkeypatch.delenv("FMX_GROUPED")
             monkeypatch.setenv("FMX_GROUPED_MIN", "100000")
         ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
         info = ix.info()
@@ -153,3 +160,20 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
     orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
     ooff, olocs = orc.locate_batch(data, offsets)
     assert np.array_equal(res[None][0], ooff) and np.array_equal(res[None][1], olocs)
+
+
+def test_default_policy_by_alphabet(pkg, O, monkeypatch):
+    """Grouping is on by default where the key spans at least 5 symbols
+    (ACGT: 6) and off for a 20-residue alphabet (key of 2 symbols)."""
+    monkeypatch.delenv("FMX_GROUPED", raising=False)
+    monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
+    rng = np.random.default_rng(9)
+    for chars, want_len, on in ((b"ACGT", 6, True), (b"ACDEFGHIKLMNPQRSTVWY", 2, False)):
+        table = table_from_symbols([bytes([c]) for c in chars])
+        text = rand_text(rng, chars, 20_000, 20_000)
+        blob = T.gpu_build(pkg, text, len(chars), 4, 5, 64, 2, 2, table)
+        ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block5(pkg.Vector.U64), options=1)
+        info = ix.info()
+        assert info["group_key_len"] == want_len and info["group_key_base"] == len(chars)
+        assert (info["grouped_min"] == 131072) == on
+        ix.close()
