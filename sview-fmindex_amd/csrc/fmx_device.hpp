@@ -365,6 +365,23 @@ struct Occ {
         rhi = rh.ck + (P)rh.pl.rank((uint32_t)((uint64_t)phi % VB), c);
     }
 
+    // A one-line symbol-mask record's get_pre_rank_and_symidx from its chunks:
+    // the symbol is the unit whose mask holds the position.
+    FMX_HD static P pre_rank_sym_from(const V4 (&ch)[NCH > 0 ? NCH : 1], uint32_t rem, uint32_t sigma, uint32_t &c) {
+        Hot hs[NCK2];
+        c = 0;
+#pragma unroll
+        for (int i = 0; i < NCK2; ++i) {
+            uint32_t d[U / 4 > 0 ? U / 4 : 1];
+#pragma unroll
+            for (int j = 0; j < U / 4; ++j) d[j] = i < NCK ? dw(ch, i * (U / 4) + j) : 0u;
+            hs[i] = hot_from(d);
+            if (i < NCK && (uint32_t)i < sigma && hot_bit(hs[i], rem)) c = (uint32_t)i;
+        }
+        const Hot h = tree_pick<NCK2>(hs, c);
+        return hot_occ(h, rem);
+    }
+
     // get_pre_rank_and_symidx body (bwm/mod.rs:223-235) for stored position p:
     // the symbol is only known after the planes arrive, so every checkpoint
     // slot of the block is fetched alongside them (one round trip) and the
@@ -404,18 +421,7 @@ struct Occ {
                 ch[i] = rp[i];
 #endif
             }
-            Hot hs[NCK2];
-            c = 0;
-#pragma unroll
-            for (int i = 0; i < NCK2; ++i) {
-                uint32_t d[U / 4];
-#pragma unroll
-                for (int j = 0; j < U / 4; ++j) d[j] = i < NCK ? dw(ch, i * (U / 4) + j) : 0u;
-                hs[i] = hot_from(d);
-                if (i < NCK && (uint32_t)i < a.sigma && hot_bit(hs[i], rem)) c = (uint32_t)i;
-            }
-            const Hot h = tree_pick<NCK2>(hs, c);
-            return hot_occ(h, rem);
+            return pre_rank_sym_from(ch, rem, a.sigma, c);
         } else {
             const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB);
             V4 ch[NCH];
@@ -963,5 +969,168 @@ FMX_HD P walk_row(const QueryArgs &a, const P *C, P pos) {
     return load_once(reinterpret_cast<const P *>(a.sa) + slot) + off;
 }
 
+
+// ------------------------------------------- two patterns per lane (grouped)
+
+// The faithful search (search_seeded, VAR 0: seed count_array.rs:203-233,
+// LF loop with_slice.rs:27-31, next_pos_range locate/mod.rs:39-45) of two
+// patterns advanced in lockstep by one lane, so that every LF step has both
+// chains' record loads in flight at once (symbol-mask records: both fetched,
+// then both ranked).  live[q] = false: no pattern (lo = hi = 0).
+template <typename P, int N, int VB, int REC>
+FMX_HD void search_pair(const QueryArgs &a, const Tables<P> &s, const PatView (&pv)[2], const bool (&live)[2],
+                        P (&lo)[2], P (&hi)[2], uint32_t (&bad)[2]) {
+    using O = Occ<P, N, VB, REC>;
+    const uint32_t sigma = a.sigma, k = a.k;
+    const P sent = (P)a.sentinel;
+    uint64_t idx[2];
+    uint32_t c[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        lo[q] = hi[q] = 0;
+        bad[q] = 0;
+        idx[q] = 0;
+        c[q] = 0;
+        if (!live[q]) continue;
+        const uint64_t m = pv[q].m;
+        if (m == 0) {
+            bad[q] = kStatusEmpty;  // count_array.rs:211 panics on an empty pattern
+            continue;
+        }
+        uint64_t code = 0, e;
+        const uint64_t take = m < k ? m : k, first = m < k ? 0 : m - k;
+        uint32_t b = 0;
+        for (uint64_t j = 0; j < take; ++j) {
+            const uint32_t cj = pv[q].at(first + j);
+            b |= cj >= sigma;
+            code += (uint64_t)(cj + 1) * s.mult[j];
+        }
+        if (b) {
+            bad[q] = kStatusSymbol;
+            continue;
+        }
+        if (m < k) { e = code + s.mult[m - 1] - 1; idx[q] = 0; }
+        else { e = code; idx[q] = m - k; }
+        lo[q] = s.kt[code - 1];
+        hi[q] = s.kt[e];
+        c[q] = idx[q] > 0 ? pv[q].at(idx[q] - 1) : 0;
+    }
+    for (;;) {
+        bool act[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            act[q] = lo[q] < hi[q] && idx[q] > 0;
+            if (act[q] && c[q] >= sigma) {
+                lo[q] = hi[q] = 0;
+                bad[q] = kStatusSymbol;
+                act[q] = false;
+            }
+        }
+        if (!act[0] && !act[1]) break;
+        P plo[2], phi[2], rlo[2], rhi[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            plo[q] = lo[q] + (lo[q] < sent ? P(1) : P(0));  // bwm/mod.rs:202-204
+            phi[q] = hi[q] + (hi[q] < sent ? P(1) : P(0));
+        }
+        if constexpr (O::ONEHOT) {
+            typename O::Hot hl[2], hh[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (!act[q]) continue;
+                const uint64_t ql = (uint64_t)plo[q] / VB, qh = (uint64_t)phi[q] / VB;
+                hl[q] = O::hot_fetch(a, ql, c[q]);
+                hh[q] = hl[q];
+                if (qh != ql) hh[q] = O::hot_fetch(a, qh, c[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (!act[q]) continue;
+                rlo[q] = O::hot_occ(hl[q], (uint32_t)((uint64_t)plo[q] % VB));
+                rhi[q] = O::hot_occ(hh[q], (uint32_t)((uint64_t)phi[q] % VB));
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (act[q]) O::rank_pair(a, plo[q], phi[q], c[q], rlo[q], rhi[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (!act[q]) continue;
+            idx[q] -= 1;
+            const P pre = s.C[c[q]];
+            c[q] = idx[q] > 0 ? pv[q].at(idx[q] - 1) : 0;
+            lo[q] = pre + rlo[q];
+            hi[q] = pre + rhi[q];
+        }
+    }
+}
+
+// walk_row for two rows of one lane in lockstep (locate/mod.rs:19-35,
+// suffix_array/mod.rs:100-105); live[q] = false: no row.
+template <typename P, int N, int VB, int REC>
+FMX_HD void walk_pair(const QueryArgs &a, const P *C, P (&pos)[2], const bool (&live)[2], P (&loc)[2]) {
+    using O = Occ<P, N, VB, REC>;
+    const P sent = (P)a.sentinel;
+    P off[2] = {P(0), P(0)};
+    uint64_t rem[2], slot[2];
+    bool w[2], top[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        slot[q] = sr_div(a, (uint64_t)pos[q], rem[q]);
+        w[q] = live[q] && rem[q] != 0;
+        top[q] = false;
+        loc[q] = 0;
+    }
+    while (w[0] || w[1]) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (w[q] && pos[q] == (P)(sent - P(1))) {  // get_pre_rank_and_symidx -> None
+                loc[q] = off[q];
+                w[q] = false;
+                top[q] = true;
+            }
+        P rank[2];
+        uint32_t cc[2];
+        if constexpr (O::ONEHOT && !O::MULTI) {
+            V4 ch[2][O::NCH];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (!w[q]) continue;
+                const P p = pos[q] + (pos[q] < sent ? P(1) : P(0));
+                const V4 *rp = reinterpret_cast<const V4 *>(a.occ + ((uint64_t)p / VB) * O::RB);
+#pragma unroll
+                for (int i = 0; i < O::NCH; ++i) ch[q][i] = rp[i];
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (!w[q]) continue;
+                const P p = pos[q] + (pos[q] < sent ? P(1) : P(0));
+                rank[q] = O::pre_rank_sym_from(ch[q], (uint32_t)((uint64_t)p % VB), a.sigma, cc[q]);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (!w[q]) continue;
+                const P p = pos[q] + (pos[q] < sent ? P(1) : P(0));
+                rank[q] = O::pre_rank_sym(a, p, cc[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (!w[q]) continue;
+            pos[q] = C[cc[q]] + rank[q];
+            off[q] += 1;
+            slot[q] = sr_div(a, (uint64_t)pos[q], rem[q]);
+            w[q] = rem[q] != 0;
+        }
+    }
+    P v[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) v[q] = live[q] && !top[q] ? load_once(reinterpret_cast<const P *>(a.sa) + slot[q]) : P(0);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (live[q] && !top[q]) loc[q] = v[q] + off[q];
+}
 
 }  // namespace fmx

@@ -153,6 +153,7 @@ struct fmx_index {
     uint64_t grouped_min = 0;
     uint32_t gkey_len = 0, gkey_base = 0;
     uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
+    uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -264,7 +265,7 @@ struct LayoutOps {
                        uint32_t fold, hipStream_t s);
     // grouped launch (faithful variant): k_search_grouped over `total` patterns in key order
     hipError_t (*search_grouped)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
-                                 uint64_t total, uint32_t cap, uint32_t xcd, hipStream_t s);
+                                 uint64_t total, uint32_t cap, uint32_t pair, uint32_t xcd, hipStream_t s);
     hipError_t (*dlut_level)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
                              void *child, hipStream_t s);
     hipError_t (*full_sa)(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t n, void *sa_out,

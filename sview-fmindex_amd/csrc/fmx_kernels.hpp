@@ -541,16 +541,36 @@ struct GroupBatch {
 };
 
 // 3. Search the launch's patterns in key order: workgroup b takes sorted
-// positions [256 b, 256 b + 256) — their records are read in order, the
-// symbols unpacked into each lane's cap bytes of LDS — searches, walks a single
-// row, and leaves its record at the pattern's own index.
-template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256, 8) void k_search_grouped(const QueryArgs a, const LocateGroup grp,
+// positions [256 K b, 256 K (b + 1)), K = 1 or 2 patterns per lane (lane t:
+// positions 256 K b + t + 256 j) — their records are read in order, the
+// symbols unpacked into cap bytes of LDS per pattern — searches (K = 2: both
+// chains in lockstep, search_pair), walks a single row, and leaves each
+// record at its pattern's own index.
+template <typename P>
+__device__ __forceinline__ void grouped_unpack(const U4 &e, uint32_t m, uint32_t bits, uint8_t *dst) {
+    const uint32_t msk = (1u << bits) - 1u;
+    const uint64_t lo = (uint64_t)e.x | ((uint64_t)e.y << 32), hi = e.z;
+    for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t at = j * bits;
+        uint64_t x;
+        if (at < 64) {
+            x = lo >> at;
+            if (at + bits > 64) x |= hi << (64 - at);
+        } else {
+            x = hi >> (at - 64);
+        }
+        dst[j] = (uint8_t)(x & msk);
+    }
+}
+
+template <typename P, int N, int VB, int REC, int K>
+__global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const QueryArgs a, const LocateGroup grp,
                                                            uint64_t total, uint32_t cap, uint32_t xcd) {
+    static_assert(K == 1 || K == 2, "one or two patterns per lane");
     __shared__ Tables<P> s;
     __shared__ GroupBatch<P> sb[kMaxGroup];
-    extern __shared__ uint8_t s_pat[];  // 256 x cap B of symbols (cap >= every batch's length), then the k-mer table
-    stage_tables(a, s, s_pat + 256 * cap);
+    extern __shared__ uint8_t s_pat[];  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
+    stage_tables(a, s, s_pat + 256 * K * cap);
     if (threadIdx.x == 0) {
         uint64_t pend = 0;
         for (uint32_t j = 0; j < grp.n; ++j) {
@@ -574,46 +594,74 @@ __global__ __launch_bounds__(256, 8) void k_search_grouped(const QueryArgs a, co
         const uint32_t q = gridDim.x / 8, rem = gridDim.x % 8, x = blockIdx.x % 8;
         chunk = x * q + (x < rem ? x : rem) + blockIdx.x / 8;
     }
-    const uint64_t sp = (uint64_t)chunk * 256u + threadIdx.x;
-    if (sp >= total) return;
-    uint32_t js = 0;
-    for (uint32_t t = 0; t + 1 < grp.n; ++t) js += sp >= sb[t].pend ? 1u : 0u;
-    const U4 e = sb[js].sorted[sp - (sb[js].pend - sb[js].npat)];
-    const uint32_t v = e.w;
-    uint32_t jb = 0;
-    for (uint32_t t = 1; t < grp.n; ++t) jb += (v >> 8) >= sb[t].tile_begin ? 1u : 0u;
-    const GroupBatch<P> &B = sb[jb];
-    const uint64_t i = (uint64_t)(v - B.tile_begin * 256u);
-    const uint32_t m = B.stride, bits = grp.gbits, msk = (1u << bits) - 1u;
-    uint8_t *dst = s_pat + threadIdx.x * cap;
-    const uint64_t lo = (uint64_t)e.x | ((uint64_t)e.y << 32), hi = e.z;
-    for (uint32_t j = 0; j < m; ++j) {
-        const uint32_t at = j * bits;
-        uint64_t x;
-        if (at < 64) {
-            x = lo >> at;
-            if (at + bits > 64) x |= hi << (64 - at);
-        } else {
-            x = hi >> (at - 64);
+    PatView pv[K];
+    bool live[K];
+    uint64_t pi[K];
+    uint32_t pj[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        const uint64_t sp = (uint64_t)chunk * (256u * K) + (uint32_t)q * 256u + threadIdx.x;
+        live[q] = sp < total;
+        pi[q] = 0;
+        pj[q] = 0;
+        uint8_t *dst = s_pat + ((uint32_t)q * 256u + threadIdx.x) * cap;
+        pv[q].m = 0;
+        pv[q].rev = false;
+        pv[q].raw = nullptr;
+        pv[q].enc = s.enc;
+        pv[q].sym = dst;
+        if (!live[q]) continue;
+        uint32_t js = 0;
+        for (uint32_t t = 0; t + 1 < grp.n; ++t) js += sp >= sb[t].pend ? 1u : 0u;
+        const U4 e = sb[js].sorted[sp - (sb[js].pend - sb[js].npat)];
+        const uint32_t v = e.w;
+        uint32_t jb = 0;
+        for (uint32_t t = 1; t < grp.n; ++t) jb += (v >> 8) >= sb[t].tile_begin ? 1u : 0u;
+        pj[q] = jb;
+        pi[q] = (uint64_t)(v - sb[jb].tile_begin * 256u);
+        pv[q].m = sb[jb].stride;
+        grouped_unpack<P>(e, sb[jb].stride, grp.gbits, dst);
+    }
+    P lo_r[K], hi_r[K], rloc[K];
+    uint64_t mask[K];
+    uint32_t mode[K];
+    if constexpr (K == 1) {
+        if (!live[0]) return;
+        const uint32_t bad = search<P, N, VB, REC, kVarFaithful>(a, s, pv[0], lo_r[0], hi_r[0], rloc[0], mask[0],
+                                                                  mode[0]);
+        if (bad) atomicOr(a.status, bad);
+        if (mode[0] == kHitRows && hi_r[0] - lo_r[0] == P(1)) {
+            rloc[0] = walk_row<P, N, VB, REC>(a, s.C, lo_r[0]);
+            mode[0] = kHitOne;
         }
-        dst[j] = (uint8_t)(x & msk);
+    } else {
+        uint32_t bad[2];
+        search_pair<P, N, VB, REC>(a, s, pv, live, lo_r, hi_r, bad);
+        if (bad[0] | bad[1]) atomicOr(a.status, bad[0] | bad[1]);
+        bool one[2];
+        P row[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            mode[q] = kHitRows;
+            mask[q] = 0;
+            rloc[q] = 0;
+            one[q] = live[q] && hi_r[q] - lo_r[q] == P(1);
+            row[q] = lo_r[q];
+        }
+        if (one[0] || one[1]) {
+            P loc[2];
+            walk_pair<P, N, VB, REC>(a, s.C, row, one, loc);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (one[q]) {
+                    rloc[q] = loc[q];
+                    mode[q] = kHitOne;
+                }
+        }
     }
-    PatView pv;
-    pv.m = m;
-    pv.rev = false;
-    pv.raw = nullptr;
-    pv.enc = s.enc;
-    pv.sym = dst;
-    P lo_r, hi_r, rloc;
-    uint64_t mask;
-    uint32_t mode;
-    const uint32_t bad = search<P, N, VB, REC, kVarFaithful>(a, s, pv, lo_r, hi_r, rloc, mask, mode);
-    if (bad) atomicOr(a.status, bad);
-    if (mode == kHitRows && hi_r - lo_r == P(1)) {
-        rloc = walk_row<P, N, VB, REC>(a, s.C, lo_r);
-        mode = kHitOne;
-    }
-    B.recs[i] = pack_rec<P>(lo_r, hi_r, rloc, mask, mode);
+#pragma unroll
+    for (int q = 0; q < K; ++q)
+        if (live[q]) sb[pj[q]].recs[pi[q]] = pack_rec<P>(lo_r[q], hi_r[q], rloc[q], mask[q], mode[q]);
 }
 
 // 3. Output offsets (tile offset + in-tile scan) and every location, rows

@@ -110,12 +110,18 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 }
 
 [[maybe_unused]] hipError_t op_search_grouped(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
-                                              uint64_t total, uint32_t cap, uint32_t xcd, hipStream_t s) {
+                                              uint64_t total, uint32_t cap, uint32_t pair, uint32_t xcd,
+                                              hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
-        const uint64_t grid = (total + 255) / 256;
+        const uint32_t per = pair ? 512u : 256u;
+        const uint64_t grid = (total + per - 1) / per;
         if (grid == 0 || grid > 0x7FFFFFFFull || cap == 0 || cap > kGroupPackBits) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_search_grouped<P, N, VB, R>), dim3((uint32_t)grid), dim3(256), 256 * cap + qa.kt_lds_bytes,
-                           s, qa, grp, total, cap, xcd);
+        if (pair)
+            hipLaunchKernelGGL((k_search_grouped<P, N, VB, R, 2>), dim3((uint32_t)grid), dim3(256),
+                               512 * cap + qa.kt_lds_bytes, s, qa, grp, total, cap, xcd);
+        else
+            hipLaunchKernelGGL((k_search_grouped<P, N, VB, R, 1>), dim3((uint32_t)grid), dim3(256),
+                               256 * cap + qa.kt_lds_bytes, s, qa, grp, total, cap, xcd);
         return hipGetLastError();
     });
 }

@@ -306,7 +306,8 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     // each lane unpacks its pattern into `cap` bytes of LDS: the longest batch's length, 4-byte aligned
     uint32_t cap = 4;
     for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
-    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_xcd, stream)) != hipSuccess)
+    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair, ix->grouped_xcd, stream)) !=
+        hipSuccess)
         return e;
     if (p4)
         hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(tiles), dim3(256), 0, stream, grp, tiles);
