@@ -227,7 +227,7 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
  * [256 B][16 KiB of key counters][tile counts][tile offsets][one search
- * record per pattern][key, place and two 16-B records per pattern].  A
+ * record per pattern][one 16-B sorted-order record per pattern].  A
  * workspace is zeroed by the caller before its first use, then belongs to
  * this index: its launches are ordered on one stream at a time (every launch
  * leaves the key counters zero again).  A locate is k_search + k_emit.  A

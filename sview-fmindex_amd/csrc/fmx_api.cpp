@@ -883,10 +883,9 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 
 // Locate workspace (fmx_internal.hpp, kWsHeader): [256 B reserved][group
 // key counters][tile counts: G][tile offsets: G][search records: n x
-// locate_rec_bytes(P)][keys][slots][sorted order], G = ceil(n / 256).
+// locate_rec_bytes(P)][sorted order: n x 16 B], G = ceil(n / 256).
 static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) {
-    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes) +
-           ((2 * n + 15) & ~15ull) + ((4 * n + 15) & ~15ull) + 32 * n;
+    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes) + 16 * n;
 }
 
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {

@@ -240,13 +240,12 @@ constexpr uint64_t kFoldTiles = 2048;
 // Locate workspace of a batch of n patterns (G = ceil(n / 256), R =
 // locate_rec_bytes):
 //   [256 B header][kGroupCounterRoom u32 key counters][tile counts: G][tile
-//   offsets: G][search records: n x R][keys: n x u16][places: n x u32]
-//   (each padded to 16 B)[packed patterns: n x 16 B][sorted order: n x 16 B]
+//   offsets: G][search records: n x R][its share of the sorted order: n x 16 B]
 // The counters sit at a fixed offset so that every launch on a workspace
 // finds them zero whatever its n.
 constexpr uint32_t kGroupKeyBits = 12;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
-constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key workgroup
+constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key / place workgroup
 constexpr uint32_t kGroupPackBits = 96;
 constexpr uint32_t kGroupCounterRoom = kGroupBins;
 constexpr uint64_t kWsHeader = 256 + 4ull * kGroupCounterRoom;

@@ -379,32 +379,20 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
 }
 
 // ---------------------------------------------------------- grouped launches
-// (fmx_internal.hpp, kWsHeader) k_group_key (one workgroup per chunk of
-// kGroupChunkTiles tiles), k_group_scan and k_group_place deal the launch's
-// patterns out in the order of their keys, each carrying its packed symbols;
-// k_search_grouped searches them in that order and writes each result at
-// the pattern's own index; k_group_tiles sums each tile's counts for k_emit.
-// No workgroup waits on another.
+// (fmx_internal.hpp, kWsHeader) k_group_key<count> (one workgroup per chunk
+// of kGroupChunkTiles tiles), k_group_scan and k_group_key<place> deal the
+// launch's patterns out in the order of their keys, each carrying its packed
+// symbols; k_search_grouped searches them in that order and writes each
+// result at the pattern's own index; k_group_tiles sums each tile's counts
+// for k_emit.  No workgroup waits on another.
 
 using U4 = uint32_t __attribute__((ext_vector_type(4)));
 
-// A batch's grouping arrays, after its search records.
-struct GroupArrays {
-    uint16_t *keys;
-    uint32_t *slots;      // the pattern's place among the launch's patterns with its key
-    U4 *packed, *sorted;  // {symbols: 96 bits, pattern id}
-};
-__device__ __forceinline__ GroupArrays group_arrays(const LocateBatch &B, uint32_t rec_bytes) {
+// A batch's share of the launch's sorted order ({symbols: 96 bits, pattern
+// id} per position), after its search records.
+__device__ __forceinline__ U4 *group_sorted(const LocateBatch &B, uint32_t rec_bytes) {
     const uint64_t n = B.npat, G = (n + 255) / 256;
-    uint8_t *p = reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + n * rec_bytes;
-    GroupArrays w;
-    w.keys = reinterpret_cast<uint16_t *>(p);
-    p += (2 * n + 15) & ~15ull;
-    w.slots = reinterpret_cast<uint32_t *>(p);
-    p += (4 * n + 15) & ~15ull;
-    w.packed = reinterpret_cast<U4 *>(p);
-    w.sorted = w.packed + n;
-    return w;
+    return reinterpret_cast<U4 *>(reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + n * rec_bytes);
 }
 
 // This workgroup's batch of a key launch (workgroup-uniform).
@@ -416,26 +404,34 @@ __device__ __forceinline__ uint32_t group_chunk_batch(const LocateGroup &grp, ui
     return jb;
 }
 
-// 1. Per chunk of kGroupChunkTiles tiles (1,024 threads, four patterns each,
-// fixed length m <= 4 W - 3 bytes): each pattern's bytes as W aligned words
+// Per chunk of kGroupChunkTiles tiles (1,024 threads, four patterns each,
+// fixed length m <= 4 W - 3 bytes), each pattern's bytes as W aligned words
 // straight into registers (consecutive patterns lie back to back, so a wave's
-// loads are contiguous); its key — its last gkey_len symbols as digits over
-// the symbols that occur in the text, the last symbol most significant (the
-// order in which the backward search reads them) — and its symbols packed
-// gbits each (a symbol >= sigma kept as sigma: the search rejects it the same
-// way), decoded byte by byte with compile-time register indices; its rank
-// among the chunk's patterns with that key (LDS histogram); then one global
-// add per key reserves the chunk's places among the launch's patterns with
-// that key, and each pattern's place (the chunk's base + its rank) is
-// written.  The offsets are checked against the length hint here (the
-// grouped search never reads them).
-template <int W>
-__global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
+// loads are contiguous), decoded byte by byte at compile-time register
+// indices into its key — its last gkey_len symbols as digits over the
+// symbols that occur in the text, the last symbol most significant (the
+// order in which the backward search reads them) — and, when placing, its
+// symbols packed gbits each (a symbol >= sigma kept as sigma: the search
+// rejects it the same way).  An LDS histogram gives the chunk's count per
+// key and each pattern's rank among them.
+//   PLACE = false (1. count): the chunk's counts are added to the launch's
+//     (gcount); the offsets are checked against the length hint here (the
+//     grouped search never reads them).
+//   PLACE = true (3. place, after k_group_scan turned the counts into each
+//     key's first position): one returning add per key reserves the chunk's
+//     positions, and each pattern's packed record, tagged with its pattern id
+//     (tile_begin * 256 + index), is written at its sorted position (chunk
+//     base + rank) — the sorted order is held by the batches one after
+//     another.
+template <int W, bool PLACE>
+__global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
     constexpr uint32_t T = 1024, PPT = kGroupChunkTiles * 256 / T;  // patterns per thread
     __shared__ uint8_t s_enc[256];
     __shared__ uint8_t s_dig[kMaxSigma];
     __shared__ uint32_t s_pw[32];
     __shared__ uint32_t hist[kGroupBins];
+    __shared__ U4 *s_sorted[kMaxGroup];
+    __shared__ uint64_t s_pend[kMaxGroup];
     const uint32_t t = threadIdx.x;
     if (t < 256) s_enc[t] = a.enc[t];
     if (t < (uint32_t)kMaxSigma) s_dig[t] = a.dlut_dig[t] == kNoDigit ? 0 : a.dlut_dig[t];  // (absent: occurs nowhere)
@@ -445,6 +441,14 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
             s_pw[e] = w;  // base^e while it fits the key
             w = e + 1 < grp.gkey_len ? w * grp.gkey_base : w;
         }
+        if (PLACE) {
+            uint64_t pend = 0;
+            for (uint32_t j = 0; j < grp.n; ++j) {
+                pend += grp.b[j].npat;
+                s_sorted[j] = group_sorted(grp.b[j], rec_bytes);
+                s_pend[j] = pend;
+            }
+        }
     }
     for (uint32_t x = t; x < kGroupBins; x += T) hist[x] = 0;
     __syncthreads();
@@ -453,11 +457,11 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
     const uint64_t n = B.npat, first = (uint64_t)(c - grp.chunk_begin[jb]) * kGroupChunkTiles * 256u;
     const uint32_t m = B.stride, bits = grp.gbits, sym_max = a.sigma, L = grp.gkey_len;
     const bool rev = B.rev != 0;
-    const GroupArrays w = group_arrays(B, rec_bytes);
-    if (first == 0 && t == 0 && B.offs[0] != 0) atomicOr(a.status, kStatusStride);
+    if (!PLACE && first == 0 && t == 0 && B.offs[0] != 0) atomicOr(a.status, kStatusStride);
     // G patterns' words in flight at once (all of a thread's when they are short)
     constexpr uint32_t G = W <= 8 ? PPT : 1;
     uint32_t key_r[PPT], rank_r[PPT];
+    U4 rec_r[PLACE ? PPT : 1];
 #pragma unroll
     for (uint32_t p0 = 0; p0 < PPT; p0 += G) {
     uint32_t x[G][W], lead[G];
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
         const bool ok = i < n;
 #pragma unroll
         for (uint32_t q = 0; q < W; ++q) x[g][q] = ok && 4 * q < lead[g] + m ? src[q] : 0u;
-        chk[g] = ok ? B.offs[i + 1] : 0;
+        chk[g] = ok && !PLACE ? B.offs[i + 1] : 0;
     }
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
         const uint64_t i = first + p * T + t;
         key_r[p] = rank_r[p] = 0;
         if (i >= n) continue;
-        if (chk[g] != (i + 1) * m) atomicOr(a.status, kStatusStride);
+        if (!PLACE && chk[g] != (i + 1) * m) atomicOr(a.status, kStatusStride);
         uint64_t lo = 0, hi = 0;
         uint32_t key = 0;
 #pragma unroll
@@ -490,42 +494,57 @@ __global__ __launch_bounds__(1024) void k_group_key(const QueryArgs a, const Loc
             uint32_t cj = s_enc[(x[g][b >> 2] >> (8 * (b & 3))) & 0xffu];
             const uint32_t back = m - 1 - j;  // 0 = the last symbol
             if (back < L) key += (cj < (uint32_t)kMaxSigma ? s_dig[cj] : 0u) * s_pw[L - 1 - back];
-            cj = cj < sym_max ? cj : sym_max;
-            const uint32_t at = j * bits;
-            if (at < 64) {
-                lo |= (uint64_t)cj << at;
-                if (at + bits > 64) hi |= (uint64_t)cj >> (64 - at);
-            } else {
-                hi |= (uint64_t)cj << (at - 64);
+            if constexpr (PLACE) {
+                cj = cj < sym_max ? cj : sym_max;
+                const uint32_t at = j * bits;
+                if (at < 64) {
+                    lo |= (uint64_t)cj << at;
+                    if (at + bits > 64) hi |= (uint64_t)cj >> (64 - at);
+                } else {
+                    hi |= (uint64_t)cj << (at - 64);
+                }
             }
         }
         key_r[p] = key;
-        rank_r[p] = atomicAdd(&hist[key], 1u);
-        U4 e;
-        e.x = (uint32_t)lo;
-        e.y = (uint32_t)(lo >> 32);
-        e.z = (uint32_t)hi;
-        e.w = 0u;
-        w.packed[i] = e;
+        if constexpr (PLACE) {
+            rank_r[p] = atomicAdd(&hist[key], 1u);
+            rec_r[p].x = (uint32_t)lo;
+            rec_r[p].y = (uint32_t)(lo >> 32);
+            rec_r[p].z = (uint32_t)hi;
+            rec_r[p].w = (uint32_t)(grp.tile_begin[jb] * 256ull + i);
+        } else {
+            atomicAdd(&hist[key], 1u);
+        }
     }
     }
     __syncthreads();
-    // every add of a thread in flight at once
     constexpr uint32_t per = kGroupBins / T;
-    uint32_t h[per], base[per];
+    if constexpr (!PLACE) {
+        // the chunk's counts into the launch's
 #pragma unroll
-    for (uint32_t u = 0; u < per; ++u) h[u] = hist[u * T + t];
+        for (uint32_t u = 0; u < per; ++u) {
+            const uint32_t h = hist[u * T + t];
+            if (h) atomicAdd(grp.gcount + u * T + t, h);
+        }
+        return;
+    } else {
+        // every returning add of a thread in flight at once
+        uint32_t h[per], base[per];
 #pragma unroll
-    for (uint32_t u = 0; u < per; ++u) base[u] = h[u] ? atomicAdd(grp.gcount + u * T + t, h[u]) : 0u;
+        for (uint32_t u = 0; u < per; ++u) h[u] = hist[u * T + t];
 #pragma unroll
-    for (uint32_t u = 0; u < per; ++u) hist[u * T + t] = base[u];  // the chunk's base for each key
-    __syncthreads();
+        for (uint32_t u = 0; u < per; ++u) base[u] = h[u] ? atomicAdd(grp.gcount + u * T + t, h[u]) : 0u;
 #pragma unroll
-    for (uint32_t p = 0; p < PPT; ++p) {
-        const uint64_t i = first + p * T + t;
-        if (i < n) {
-            w.keys[i] = (uint16_t)key_r[p];
-            w.slots[i] = hist[key_r[p]] + rank_r[p];
+        for (uint32_t u = 0; u < per; ++u) hist[u * T + t] = base[u];  // the chunk's first position per key
+        __syncthreads();
+#pragma unroll
+        for (uint32_t p = 0; p < PPT; ++p) {
+            const uint64_t i = first + p * T + t;
+            if (i >= n) continue;
+            const uint64_t sp = (uint64_t)hist[key_r[p]] + rank_r[p];
+            uint32_t js = 0;
+            for (uint32_t q = 0; q + 1 < grp.n; ++q) js += sp >= s_pend[q] ? 1u : 0u;
+            s_sorted[js][sp - (js ? s_pend[js - 1] : 0)] = rec_r[p];
         }
     }
 }
@@ -578,7 +597,7 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
             const uint64_t G = (B.npat + 255) / 256;
             pend += B.npat;
             sb[j].recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
-            sb[j].sorted = group_arrays(B, sizeof(SearchRec<P>)).sorted;
+            sb[j].sorted = group_sorted(B, sizeof(SearchRec<P>));
             sb[j].npat = B.npat;
             sb[j].pend = pend;
             sb[j].tile_begin = grp.tile_begin[j];

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_scan(const LocateGroup grp) {
 }
 
 // ---------------------------------------------------------- grouped launches
-// (k_group_key, k_group_place and k_search_grouped: fmx_kernels.hpp)
+// (k_group_key<count / place> and k_search_grouped: fmx_kernels.hpp)
 
 // 2. The launch's key counts -> each key's first sorted position (exclusive
 // scan in place).
@@ -84,35 +84,6 @@ __global__ __launch_bounds__(256) void k_group_scan(uint32_t *cnt) {
         cnt[threadIdx.x * per + u] = run;
         run += v[u];
     }
-}
-
-// 3. Each pattern's sorted position (its key's first position + its place):
-// there goes its packed record, tagged with its pattern id (tile_begin * 256
-// + index).  The sorted order is held by the batches one after another.
-__global__ __launch_bounds__(256) void k_group_place(const LocateGroup grp, uint32_t rec_bytes) {
-    __shared__ U4 *s_sorted[kMaxGroup];
-    __shared__ uint64_t s_pend[kMaxGroup];
-    if (threadIdx.x == 0) {
-        uint64_t pend = 0;
-        for (uint32_t j = 0; j < grp.n; ++j) {
-            pend += grp.b[j].npat;
-            s_sorted[j] = group_arrays(grp.b[j], rec_bytes).sorted;
-            s_pend[j] = pend;
-        }
-    }
-    __syncthreads();
-    const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
-    const LocateBatch &B = grp.b[jb];
-    const uint64_t i = (uint64_t)(vt - grp.tile_begin[jb]) * 256u + threadIdx.x;
-    if (i >= B.npat) return;
-    const GroupArrays w = group_arrays(B, rec_bytes);
-    const uint64_t sp = (uint64_t)grp.gcount[w.keys[i]] + w.slots[i];
-    uint32_t js = 0;
-    for (uint32_t t = 0; t + 1 < grp.n; ++t) js += sp >= s_pend[t] ? 1u : 0u;
-    const uint64_t first = js ? s_pend[js - 1] : 0;
-    U4 e = w.packed[i];
-    e.w = vt * 256u + threadIdx.x;
-    s_sorted[js][sp - first] = e;
 }
 
 // 4. Each tile's count (k_emit's tile offsets) and each pattern's count (the
@@ -275,8 +246,8 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
     return d.ops->count(qa, d.vb, d.rec, search_var(qa, sb), d_bytes, d_offsets, n, flags, d_counts, sb, stream);
 }
 
-// A grouped launch's search (kWsHeader): keys and chunk bases, sorted order,
-// search in key order, counts.
+// A grouped launch's search (kWsHeader): key counts, their scan, the sorted
+// order, the search in key order, tile counts.
 static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
                                         uint64_t total, uint32_t sb, uint32_t bits, hipStream_t stream) {
     const Disp d = dispatch(ix);
@@ -291,17 +262,25 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     }
     const bool p4 = ix->bv.L.pos_bytes == 4;
     const uint32_t rb = (uint32_t)locate_rec_bytes(ix->bv.L.pos_bytes);
-    // the key kernel holds each pattern in W registers: 8 words up to 29 bytes, else 25 (96 bytes)
+    // the key passes hold each pattern in W registers
     uint32_t maxm = 1;
     for (uint32_t j = 0; j < grp.n; ++j) maxm = std::max<uint32_t>(maxm, grp.b[j].stride);
-    if (maxm <= 29)
-        hipLaunchKernelGGL(k_group_key<8>, dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    // (W = 6 words hold patterns up to 21 bytes at any alignment, 8 up to 29, 25 up to 97)
+    if (maxm <= 21)
+        hipLaunchKernelGGL((k_group_key<6, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    else if (maxm <= 29)
+        hipLaunchKernelGGL((k_group_key<8, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     else
-        hipLaunchKernelGGL(k_group_key<25>, dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+        hipLaunchKernelGGL((k_group_key<25, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);
-    hipLaunchKernelGGL(k_group_place, dim3(tiles), dim3(256), 0, stream, grp, rb);
+    if (maxm <= 21)
+        hipLaunchKernelGGL((k_group_key<6, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    else if (maxm <= 29)
+        hipLaunchKernelGGL((k_group_key<8, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    else
+        hipLaunchKernelGGL((k_group_key<25, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // each lane unpacks its pattern into `cap` bytes of LDS: the longest batch's length, 4-byte aligned
     uint32_t cap = 4;
