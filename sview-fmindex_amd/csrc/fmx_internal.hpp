@@ -190,7 +190,7 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                          hipStream_t stream);
 // One batch of a locate launch; a launch runs up to kMaxGroup of them, each
 // with its own patterns, outputs and workspace (fmx_locate_group_async).
-constexpr uint32_t kMaxGroup = 16;
+constexpr uint32_t kMaxGroup = 32;  // (the kernel argument then holds ~4.8 KB: gfx950 / ROCm 7 take it)
 struct LocateBatch {
     const uint8_t *bytes;
     const uint64_t *offs;

@@ -509,7 +509,7 @@ def test_locate_queue_many_launches_one_workspace(pkg, O):
 
 
 def test_locate_group_launch(pkg, O):
-    """fmx_locate_group_async: up to 16 batches per launch (more are
+    """fmx_locate_group_async: up to 32 batches per launch (more are
     split over launches), sizes from 0 to a few thousand, forward and
     reversed, each batch's outputs equal to the host API's; repeated so the
     workspaces' look-back epochs wrap; a shared workspace is rejected."""
@@ -521,7 +521,8 @@ def test_locate_group_launch(pkg, O):
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64))
     dev = torch.device("cuda:0")
     sizes = [2500, 0, 1, 700, 256, 257, 3000, 40, 1999, 5, 1024,
-             33, 600, 0, 77, 4096, 12, 300, 2, 900, 128]  # 21 batches: two launches
+             33, 600, 0, 77, 4096, 12, 300, 2, 900, 128,
+             64, 1500, 3, 255, 511, 7, 2048, 90, 0, 333, 17, 1200, 4, 640, 9, 2222, 31, 800, 65]  # 40 (38 non-empty): two launches
     bats, jobs = [], []
     for bi, n in enumerate(sizes):
         rev = bi % 3 == 2
