@@ -1,16 +1,19 @@
 // Does a kernel take an 8 KB by-value argument on this ROCm (kernarg segment limit)?
 #include <hip/hip_runtime.h>
 #include <cstdio>
-struct Big { unsigned long long v[1024]; };  // 8 KB
+#ifndef WORDS
+#define WORDS 1024
+#endif
+struct Big { unsigned long long v[WORDS]; };  // WORDS x 8 B
 __global__ void k_big(const Big b, unsigned long long *out) {
     unsigned long long s = 0;
-    for (int i = threadIdx.x; i < 1024; i += 64) s += b.v[i];
+    for (int i = threadIdx.x; i < WORDS; i += 64) s += b.v[i];
     atomicAdd(out, s);
 }
 int main() {
     Big b;
     unsigned long long want = 0;
-    for (int i = 0; i < 1024; ++i) { b.v[i] = i * 3 + 1; want += b.v[i]; }
+    for (int i = 0; i < WORDS; ++i) { b.v[i] = i * 3 + 1; want += b.v[i]; }
     unsigned long long *d = nullptr, got = 0;
     if (hipMalloc(&d, 8) != hipSuccess) return 2;
     hipMemset(d, 0, 8);

@@ -405,7 +405,8 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     memcpy(q.enc, v.enc, 256);
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
-    if (hipMemset(ix->d_status, 0, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMemsetAsync(ix->d_status, 0, kStatusSlots * 4, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+    if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
     ix->slots.assign(kStatusSlots, StatusSlot{});
     if (const char *e = getenv("FMX_SEARCH_PERSISTENT")) ix->search_persistent = e[0] == '1';
     for (uint32_t i = kStatusSlots; i-- > 0;) ix->free_slots.push_back(i);
@@ -1067,7 +1068,11 @@ static fmx_status ensure_ws(fmx_index *ix, uint64_t n) {
     ix->ws_bytes = 0;
     const uint64_t want = std::max<uint64_t>(need, 1 << 16);
     if (hipMalloc(&ix->d_ws, want) != hipSuccess) return FMX_E_DEVICE;
-    if (hipMemset(ix->d_ws, 0, want) != hipSuccess) return FMX_E_DEVICE;
+    // zeroed on the index's own (non-blocking) stream, which the host-API
+    // launches use: a plain hipMemset runs on the null stream, unordered
+    // with it, and a grouped launch's key counters must start at zero
+    if (hipMemsetAsync(ix->d_ws, 0, want, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+    if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
     ix->ws_bytes = want;
     return FMX_OK;
 }

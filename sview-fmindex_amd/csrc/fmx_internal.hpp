@@ -190,7 +190,8 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                          hipStream_t stream);
 // One batch of a locate launch; a launch runs up to kMaxGroup of them, each
 // with its own patterns, outputs and workspace (fmx_locate_group_async).
-constexpr uint32_t kMaxGroup = 32;  // (the kernel argument then holds ~4.8 KB: gfx950 / ROCm 7 take it)
+constexpr uint32_t kMaxGroup = 128;  // (the kernel argument then holds ~14 KB: gfx950 / ROCm 7 take up to 32 KB,
+                                     // scripts/micro/kernarg.hip)
 struct LocateBatch {
     const uint8_t *bytes;
     const uint64_t *offs;
@@ -203,6 +204,7 @@ struct LocateBatch {
     uint64_t *tiles;
     uint32_t rev;
     uint32_t stride;  // FMX_HINT_FIXED_LEN: offs[i] == i * stride (0: read the offsets)
+    uint64_t first;   // the launch's patterns in the batches before this one (set by launch_split)
 };
 struct LocateGroup {
     LocateBatch b[kMaxGroup];

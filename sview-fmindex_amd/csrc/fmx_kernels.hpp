@@ -290,13 +290,16 @@ __device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &
 // when launches on several streams share the CUs).  Per batch of a group:
 // workspace = [256 B][tile counts: G][tile offsets: G][search records: n].
 
-// This workgroup's batch of a grouped launch (workgroup-uniform).
+// This workgroup's batch of a grouped launch (workgroup-uniform): the last
+// batch whose first workgroup is at most vt, by binary search.
 __device__ __forceinline__ uint32_t group_batch(const LocateGroup &grp, uint32_t vt) {
-    uint32_t jb = 0;
-#pragma unroll
-    for (uint32_t t = 1; t < kMaxGroup; ++t)
-        if (t < grp.n && vt >= grp.tile_begin[t]) jb = t;
-    return jb;
+    uint32_t lo = 0, hi = grp.n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (grp.tile_begin[mid] <= vt) lo = mid;
+        else hi = mid;
+    }
+    return lo;
 }
 
 // 1. Search every pattern; its result record, its count; the tile's count.
@@ -395,13 +398,28 @@ __device__ __forceinline__ U4 *group_sorted(const LocateBatch &B, uint32_t rec_b
     return reinterpret_cast<U4 *>(reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + n * rec_bytes);
 }
 
-// This workgroup's batch of a key launch (workgroup-uniform).
+// This workgroup's batch of a key launch (workgroup-uniform, binary search).
 __device__ __forceinline__ uint32_t group_chunk_batch(const LocateGroup &grp, uint32_t c) {
-    uint32_t jb = 0;
-#pragma unroll
-    for (uint32_t t = 1; t < kMaxGroup; ++t)
-        if (t < grp.n && c >= grp.chunk_begin[t]) jb = t;
-    return jb;
+    uint32_t lo = 0, hi = grp.n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (grp.chunk_begin[mid] <= c) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// The last index j < n with key[j] <= x (key ascending, key[0] <= x): a
+// per-lane binary search over an LDS table.
+template <typename T, typename K>
+__device__ __forceinline__ uint32_t lds_upper(const T *tab, uint32_t n, K x) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tab[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
 }
 
 // Per chunk of kGroupChunkTiles tiles (1,024 threads, four patterns each,
@@ -431,8 +449,12 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     __shared__ uint32_t s_pw[32];
     __shared__ uint32_t hist[kGroupBins];
     __shared__ U4 *s_sorted[kMaxGroup];
-    __shared__ uint64_t s_pend[kMaxGroup];
+    __shared__ uint64_t s_first[kMaxGroup];
     const uint32_t t = threadIdx.x;
+    if (PLACE && t < grp.n) {
+        s_sorted[t] = group_sorted(grp.b[t], rec_bytes);
+        s_first[t] = grp.b[t].first;
+    }
     if (t < 256) s_enc[t] = a.enc[t];
     if (t < (uint32_t)kMaxSigma) s_dig[t] = a.dlut_dig[t] == kNoDigit ? 0 : a.dlut_dig[t];  // (absent: occurs nowhere)
     if (t == 0) {
@@ -440,14 +462,6 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
         for (uint32_t e = 0; e < 32; ++e) {
             s_pw[e] = w;  // base^e while it fits the key
             w = e + 1 < grp.gkey_len ? w * grp.gkey_base : w;
-        }
-        if (PLACE) {
-            uint64_t pend = 0;
-            for (uint32_t j = 0; j < grp.n; ++j) {
-                pend += grp.b[j].npat;
-                s_sorted[j] = group_sorted(grp.b[j], rec_bytes);
-                s_pend[j] = pend;
-            }
         }
     }
     for (uint32_t x = t; x < kGroupBins; x += T) hist[x] = 0;
@@ -542,9 +556,8 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
             const uint64_t i = first + p * T + t;
             if (i >= n) continue;
             const uint64_t sp = (uint64_t)hist[key_r[p]] + rank_r[p];
-            uint32_t js = 0;
-            for (uint32_t q = 0; q + 1 < grp.n; ++q) js += sp >= s_pend[q] ? 1u : 0u;
-            s_sorted[js][sp - (js ? s_pend[js - 1] : 0)] = rec_r[p];
+            const uint32_t js = lds_upper(s_first, grp.n, sp);
+            s_sorted[js][sp - s_first[js]] = rec_r[p];
         }
     }
 }
@@ -555,8 +568,7 @@ template <typename P>
 struct GroupBatch {
     SearchRec<P> *recs;
     const U4 *sorted;
-    uint64_t npat, pend;  // pend: the batches' patterns up to and including this one
-    uint32_t tile_begin, stride;
+    uint32_t stride;
 };
 
 // 3. Search the launch's patterns in key order: workgroup b takes sorted
@@ -588,21 +600,18 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     static_assert(K == 1 || K == 2, "one or two patterns per lane");
     __shared__ Tables<P> s;
     __shared__ GroupBatch<P> sb[kMaxGroup];
+    __shared__ uint64_t s_first[kMaxGroup];   // the launch's patterns before batch j
+    __shared__ uint32_t s_vfirst[kMaxGroup];  // batch j's first pattern id (tile_begin * 256)
     extern __shared__ uint8_t s_pat[];  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
     stage_tables(a, s, s_pat + 256 * K * cap);
-    if (threadIdx.x == 0) {
-        uint64_t pend = 0;
-        for (uint32_t j = 0; j < grp.n; ++j) {
-            const LocateBatch &B = grp.b[j];
-            const uint64_t G = (B.npat + 255) / 256;
-            pend += B.npat;
-            sb[j].recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
-            sb[j].sorted = group_sorted(B, sizeof(SearchRec<P>));
-            sb[j].npat = B.npat;
-            sb[j].pend = pend;
-            sb[j].tile_begin = grp.tile_begin[j];
-            sb[j].stride = B.stride;
-        }
+    for (uint32_t j = threadIdx.x; j < grp.n; j += 256) {
+        const LocateBatch &B = grp.b[j];
+        const uint64_t G = (B.npat + 255) / 256;
+        sb[j].recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
+        sb[j].sorted = group_sorted(B, sizeof(SearchRec<P>));
+        sb[j].stride = B.stride;
+        s_first[j] = B.first;
+        s_vfirst[j] = grp.tile_begin[j] * 256u;
     }
     __syncthreads();
     // xcd: workgroup b takes chunk start(b % 8) + b / 8, so that (under the
@@ -630,14 +639,12 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         pv[q].enc = s.enc;
         pv[q].sym = dst;
         if (!live[q]) continue;
-        uint32_t js = 0;
-        for (uint32_t t = 0; t + 1 < grp.n; ++t) js += sp >= sb[t].pend ? 1u : 0u;
-        const U4 e = sb[js].sorted[sp - (sb[js].pend - sb[js].npat)];
+        const uint32_t js = lds_upper(s_first, grp.n, sp);
+        const U4 e = sb[js].sorted[sp - s_first[js]];
         const uint32_t v = e.w;
-        uint32_t jb = 0;
-        for (uint32_t t = 1; t < grp.n; ++t) jb += (v >> 8) >= sb[t].tile_begin ? 1u : 0u;
+        const uint32_t jb = lds_upper(s_vfirst, grp.n, v);
         pj[q] = jb;
-        pi[q] = (uint64_t)(v - sb[jb].tile_begin * 256u);
+        pi[q] = (uint64_t)(v - s_vfirst[jb]);
         pv[q].m = sb[jb].stride;
         grouped_unpack<P>(e, sb[jb].stride, grp.gbits, dst);
     }

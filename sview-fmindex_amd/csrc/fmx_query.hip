@@ -311,7 +311,10 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
     const Disp d = dispatch(ix);
     LocateGroup grp = grp_in;
     uint64_t total = 0;
-    for (uint32_t j = 0; j < grp.n; ++j) total += grp.b[j].npat;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        grp.b[j].first = total;
+        total += grp.b[j].npat;
+    }
     const uint32_t bits = group_pack_bits(ix, grp);
     const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= ix->grouped_min && !grp.tile_ctr &&
                          search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;

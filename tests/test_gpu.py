@@ -522,7 +522,8 @@ def test_locate_group_launch(pkg, O):
     dev = torch.device("cuda:0")
     sizes = [2500, 0, 1, 700, 256, 257, 3000, 40, 1999, 5, 1024,
              33, 600, 0, 77, 4096, 12, 300, 2, 900, 128,
-             64, 1500, 3, 255, 511, 7, 2048, 90, 0, 333, 17, 1200, 4, 640, 9, 2222, 31, 800, 65]  # 40 (38 non-empty): two launches
+             64, 1500, 3, 255, 511, 7, 2048, 90, 0, 333, 17, 1200, 4, 640, 9, 2222, 31, 800, 65]
+    sizes += [int(x) for x in np.random.default_rng(5).integers(1, 600, size=100)]  # 140 (138 non-empty): two launches
     bats, jobs = [], []
     for bi, n in enumerate(sizes):
         rev = bi % 3 == 2
