@@ -509,7 +509,7 @@ def test_locate_queue_many_launches_one_workspace(pkg, O):
 
 
 def test_locate_group_launch(pkg, O):
-    """fmx_locate_group_async: up to 32 batches per launch (more are
+    """fmx_locate_group_async: up to 128 batches per launch (more are
     split over launches), sizes from 0 to a few thousand, forward and
     reversed, each batch's outputs equal to the host API's; repeated so the
     workspaces' look-back epochs wrap; a shared workspace is rejected."""
