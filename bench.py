@@ -82,16 +82,16 @@ CONFIGS = {
     "c1": dict(text_len=1_000_000, alphabet=b"ACGT", symbols=[b"Aa", b"Cc", b"Gg", b"Tt"], pos=4, planes=2,
                vec=64, k=3, sr=2, patterns=1_000, m=20, total=0, group=16, streams=8,
                desc="C1: 1 Mbp ACGT, 1,000 x 20 bp, u32/Block2<u64>, sr 2, k 3"),
-    # configs[1]: the headline (metric quoted on it).  128 batches per launch (one launch group
-    # per stream, 256 distinct batches): a grouped launch of 12.8 M patterns shares more of its
-    # first LF steps than one of 3.2 M, 1.6 M or 0.8 M (3.21 vs 2.84 vs ~2.7 vs ~2.6e9 on one box;
-    # launch order ~2.58; profiles/r3/grouped/r3ls2, r3g32, r3g6)
+    # configs[1]: the headline (metric quoted on it).  256 batches per launch (one launch group
+    # per stream, 512 distinct batches): a grouped launch of 25.6 M patterns shares more of its
+    # first LF steps than one of 12.8 M, 3.2 M, 1.6 M or 0.8 M (3.42 vs 3.28 vs 2.84 vs ~2.7 vs
+    # ~2.6e9; launch order ~2.58; profiles/r3/narrow, profiles/r3/grouped/r3ls2, r3g32, r3g6)
     "c2": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
-               patterns=100_000, m=20, total=0, group=128,
+               patterns=100_000, m=20, total=0, group=256,
                desc="C2: 1 Gbp ACGT (ACGTN, N wildcard), 100,000 x 20 bp per GPU, u32/Block3<u64>, sr 2, k 3"),
     # configs[2]: 10 M patterns sharded over the GPUs
     "c3": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
-               patterns=100_000, m=20, total=10_000_000, group=128,
+               patterns=100_000, m=20, total=10_000_000, group=256,
                desc="C3: 1 Gbp ACGT, 10,000,000 x 20 bp sharded over the GPUs, u32/Block3<u64>, sr 2, k 3"),
     # configs[3]: large-alphabet occ path
     "c4": dict(text_len=1_000_000_000, alphabet=AMINO, symbols=[bytes([c, c + 32]) for c in AMINO] + [b"Xx"],
@@ -144,7 +144,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
     ap.add_argument("--batches", type=int, default=32,
                     help="distinct batches cycled (weak-scaling configs; at least one launch group per stream)")
-    ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 128; default 8; c1: 16; c2, c3: 128)")
+    ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 256; default 8; c1: 16; c2, c3: 256)")
     ap.add_argument("--graph", action="store_true",
                     help="capture one pass (every launch, forked over the streams) in a HIP graph and replay it: "
                          "one host call per pass instead of one per launch (launch-bound configs)")
@@ -530,7 +530,7 @@ def main():
     total = args.total_patterns if args.total_patterns >= 0 else cfg["total"]
     P = cfg["pos"]
     S = max(1, args.streams or cfg.get("streams", 2))
-    GR = max(1, min(args.group or cfg.get("group", 8), 128))
+    GR = max(1, min(args.group or cfg.get("group", 8), 256))
     BLK = cfg["planes"] * cfg["vec"] // 8
     position = pkg.u32 if P == 4 else pkg.u64
     block = getattr(pkg.blocks, f"Block{cfg['planes']}")(pkg.Vector(cfg["vec"]))

@@ -271,7 +271,7 @@ typedef struct fmx_locate_job {
 
 fmx_status fmx_locate_jobs_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs);
 
-/* The same batches run together: up to 128 per kernel launch on `stream` (each
+/* The same batches run together: up to 256 per kernel launch on `stream` (each
  * batch keeps its own patterns, outputs and workspace; the jobs' own stream
  * fields are ignored), so that small batches fill the GPU the way one large
  * batch does.  The jobs' workspaces must be distinct and no two jobs may share

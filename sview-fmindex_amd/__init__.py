@@ -591,7 +591,7 @@ class FmIndex:
         _check(_n.lib().fmx_locate_jobs_async(self._h, queue, len(queue)))
 
     def locate_group_async(self, queue, stream: int = 0) -> None:
-        """Run a queue of locate batches together, up to 128 per kernel launch,
+        """Run a queue of locate batches together, up to 256 per kernel launch,
         on `stream` (fmx_locate_group_async); distinct workspaces and outputs."""
         _check(_n.lib().fmx_locate_group_async(self._h, queue, len(queue), C.c_void_p(stream) if stream else None))
 

@@ -190,8 +190,11 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
                          hipStream_t stream);
 // One batch of a locate launch; a launch runs up to kMaxGroup of them, each
 // with its own patterns, outputs and workspace (fmx_locate_group_async).
-constexpr uint32_t kMaxGroup = 128;  // (the kernel argument then holds ~14 KB: gfx950 / ROCm 7 take up to 32 KB,
-                                     // scripts/micro/kernarg.hip)
+#ifndef FMX_MAX_GROUP
+#define FMX_MAX_GROUP 256  // (build option: 128 was the round-3 default until the A/B in profiles/r3/narrow)
+#endif
+constexpr uint32_t kMaxGroup = FMX_MAX_GROUP;  // (the kernel argument then holds ~25 KB: gfx950 / ROCm 7 take up to
+                                               // 32 KB, scripts/micro/kernarg.hip)
 struct LocateBatch {
     const uint8_t *bytes;
     const uint64_t *offs;
@@ -245,7 +248,10 @@ constexpr uint64_t kFoldTiles = 2048;
 //   offsets: G][search records: n x R][its share of the sorted order: n x 16 B]
 // The counters sit at a fixed offset so that every launch on a workspace
 // finds them zero whatever its n.
-constexpr uint32_t kGroupKeyBits = 12;
+#ifndef FMX_GROUP_KEY_BITS
+#define FMX_GROUP_KEY_BITS 12  // (build option, A/B: 14 = 16,384 bins, C2 keys on 7 symbols)
+#endif
+constexpr uint32_t kGroupKeyBits = FMX_GROUP_KEY_BITS;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
 constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key / place workgroup
 constexpr uint32_t kGroupPackBits = 96;

@@ -283,6 +283,26 @@ __device__ __forceinline__ uint64_t unpack_rec(const SearchRec<P> &r, P &lo, P &
     return is_mask ? (uint64_t)__builtin_popcountll(x) : (uint64_t)r.b;
 }
 
+// A grouped launch's record (the faithful search, which walks every
+// single-row interval: a count of 1 is always kHitOne): a = rloc when b = 1,
+// else lo; b = count.  Half of SearchRec<u32> for k_group_tiles and k_emit to
+// read; it sits at the start of the batch's SearchRec slot array.
+template <typename P>
+struct NarrowRec {
+    P a, b;
+};
+
+template <typename P>
+__device__ __forceinline__ uint64_t unpack_narrow(const NarrowRec<P> &r, P &lo, P &rloc, uint64_t &mask,
+                                                  uint32_t &mode) {
+    const bool one = r.b == P(1);
+    mode = one ? kHitOne : kHitRows;
+    lo = one ? P(0) : r.a;
+    rloc = one ? r.a : P(0);
+    mask = 0ull;
+    return (uint64_t)r.b;
+}
+
 // The locate launch: k_search, (k_scan,) k_emit.
 // No workgroup ever waits on another, so nothing depends on the order or
 // placement in which workgroups are dispatched (MI355X_MICROARCH.md: HIP
@@ -687,17 +707,21 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     }
 #pragma unroll
     for (int q = 0; q < K; ++q)
-        if (live[q]) sb[pj[q]].recs[pi[q]] = pack_rec<P>(lo_r[q], hi_r[q], rloc[q], mask[q], mode[q]);
+        if (live[q])
+            reinterpret_cast<NarrowRec<P> *>(sb[pj[q]].recs)[pi[q]] =
+                NarrowRec<P>{mode[q] == kHitOne ? rloc[q] : lo_r[q], (P)(hi_r[q] - lo_r[q])};
 }
 
 // 3. Output offsets (tile offset + in-tile scan) and every location, rows
 // dealt across each wave's lanes (emit_locations).
-// fold: batches of at most kFoldTiles tiles need no k_scan: each workgroup
-// sums the counts of the tiles before its own (all final: k_search is done),
-// and the last tile writes the batch total.
+// fold bit 0: batches of at most kFoldTiles tiles need no k_scan: each
+// workgroup sums the counts of the tiles before its own (all final: k_search
+// is done), and the last tile writes the batch total.  Bit 1: the records are
+// NarrowRec (a grouped launch).
 
 template <typename P, int N, int VB, int REC>
-__global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGroup grp, uint32_t fold) {
+__global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGroup grp, uint32_t flags) {
+    const uint32_t fold = flags & 1u, narrow = flags & 2u;
     __shared__ P sC[kMaxSigma + 1];
     __shared__ uint64_t s_scan[4], s_part[4];
     if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
@@ -709,7 +733,9 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
     P lo = 0, rloc = 0;
     uint64_t mask = 0, cnt = 0;
     uint32_t mode = kHitOne;
-    if (i < npat) cnt = unpack_rec<P>(recs[i], lo, rloc, mask, mode);
+    if (i < npat)
+        cnt = narrow ? unpack_narrow<P>(reinterpret_cast<const NarrowRec<P> *>(recs)[i], lo, rloc, mask, mode)
+                     : unpack_rec<P>(recs[i], lo, rloc, mask, mode);
     // the tile's base offset (fold: the earlier tiles' counts, summed here)
     // and the exclusive scan of the counts, one barrier for both
     uint64_t part = 0;

@@ -95,13 +95,10 @@ __global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp, uint
     const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
     const LocateBatch &B = grp.b[jb];
     const uint64_t G = (B.npat + 255) / 256, g = vt - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
-    const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
+    const NarrowRec<P> *__restrict__ recs = reinterpret_cast<const NarrowRec<P> *>(B.tiles + 2 * G);
     uint64_t cnt = 0;
     if (i < B.npat) {
-        P lo, rloc;
-        uint64_t mask;
-        uint32_t mode;
-        cnt = unpack_rec<P>(recs[i], lo, rloc, mask, mode);
+        cnt = (uint64_t)recs[i].b;
         if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = (P)cnt;
     }
 #pragma unroll
@@ -328,7 +325,8 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
         hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold, stream);
+    // (k_emit's flags: bit 0 fold, bit 1 NarrowRec records from the grouped search)
+    return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold | (grouped ? 2u : 0u), stream);
 }
 
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,

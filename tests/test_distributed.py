@@ -169,11 +169,11 @@ def test_shard_partition(pkg):
             assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
 
 
-@pytest.mark.parametrize("cfg,total,gr", [("c3", 10_000_000, 128), ("c3", 10_000_000, 8), ("c5", 1_000_000, 8)])
+@pytest.mark.parametrize("cfg,total,gr", [("c3", 10_000_000, 256), ("c3", 10_000_000, 128), ("c5", 1_000_000, 8)])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_job_plan_balanced(pkg, cfg, total, gr, world):
     """Every rank gets total/N patterns (within one), in the same number of
-    launch groups of GR batches (bench.py: 128 for C3, 8 for C5); the batches
+    launch groups of GR batches (bench.py: 256 for C3, 8 for C5); the batches
     tile each rank's slab."""
     plan = pkg.distributed.JobPlan(total, world, 100_000, gr)
     per_rank = [e - s for s, e in plan.spans]

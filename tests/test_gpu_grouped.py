@@ -55,7 +55,7 @@ def test_fixed_len_grouped(pkg, O, grouped, m):
 
 
 def test_group_launch_many_batches_grouped(pkg, O, grouped):
-    """140 fixed-length batches (two launches: 128 + 12), lengths 1..32, sizes
+    """270 fixed-length batches (two launches: 256 + 14), lengths 1..32, sizes
     1..4096, every third reversed, repeated 40 times on the same workspaces
     (the key counters must come back to zero after every launch)."""
     import torch
@@ -68,7 +68,7 @@ def test_group_launch_many_batches_grouped(pkg, O, grouped):
     dev = torch.device("cuda:0")
     sizes = [2500, 1, 700, 256, 257, 3000, 40, 1999, 5, 1024, 33, 600, 77, 4096, 12, 300, 2, 900, 128, 255, 3,
              64, 1500, 3, 255, 511, 7, 2048, 90, 333, 17, 1200, 4, 640, 9, 2222, 31, 800, 65, 6]
-    sizes += [int(x) for x in np.random.default_rng(6).integers(1, 600, size=100)]
+    sizes += [int(x) for x in np.random.default_rng(6).integers(1, 600, size=230)]
     bats, jobs = [], []
     for bi, n in enumerate(sizes):
         rev, m = bi % 3 == 2, 1 + (bi * 7) % 32
