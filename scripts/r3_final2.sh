@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-3 final evidence at 256 batches per launch with 8-B grouped records:
+# the whole GPU suite, smoke, the default bench line and the driver's command,
+# C3, the launch-order leg; then the profile passes of scripts/r3_profile.sh.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/${TAG:-r3v}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || exit $?
+echo suite-ok
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || exit $?
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err || exit $?
+echo bench-ok
+B="timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-blob-layout --no-cpu"
+$B --config c3 > $O/c3_grouped.json 2> $O/c3_grouped.err || exit $?
+FMX_GROUPED=0 $B > $O/c2_order.json 2> $O/c2_order.err || exit $?
+echo ab-ok
+TAG=${PTAG:-r3w} bash scripts/r3_profile.sh || exit $?
+echo profile-ok
