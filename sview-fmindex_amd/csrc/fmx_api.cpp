@@ -403,7 +403,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     memcpy(q.C, v.C, sizeof(q.C));
     memcpy(q.mult, v.mult, sizeof(q.mult));
     memcpy(q.enc, v.enc, 256);
-    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
+    if (!ix->stream && hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     if (hipMemsetAsync(ix->d_status, 0, kStatusSlots * 4, ix->stream) != hipSuccess) return FMX_E_DEVICE;
     if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
@@ -566,6 +566,7 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
     if (st & kStatusStride) return FMX_E_ARG;
+    if (st & kStatusGroup) return FMX_E_DEVICE;
     return FMX_OK;
 }
 
@@ -632,7 +633,15 @@ fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, i
         return FMX_E_DEVICE;
     }
     tr.mark("hipMalloc blob");
-    if (hipMemcpy(ix->d_blob_owned, blob, blob_len, hipMemcpyHostToDevice) != hipSuccess) {
+    // On the index's own stream, waited for: a plain hipMemcpy from pageable
+    // memory may return before its DMA lands, and the load's kernels (the
+    // record re-layout reads the blob) run on this non-blocking stream, which
+    // is not ordered after the null stream — they could read the allocation's
+    // previous contents (intermittent wrong counts with
+    // interleaved records only; reproduced by tests/test_simt.py)
+    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMemcpyAsync(ix->d_blob_owned, blob, blob_len, hipMemcpyHostToDevice, ix->stream) != hipSuccess ||
+        hipStreamSynchronize(ix->stream) != hipSuccess) {
         fmx_free(ix);
         return FMX_E_DEVICE;
     }
@@ -884,9 +893,9 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 
 // Locate workspace (fmx_internal.hpp, kWsHeader): [256 B reserved][group
 // key counters][tile counts: G][tile offsets: G][search records: n x
-// locate_rec_bytes(P)][sorted order: n x 16 B], G = ceil(n / 256).
+// locate_rec_bytes(P)][to 16 B][sorted order: n x 16 B], G = ceil(n / 256).
 static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) {
-    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes) + 16 * n;
+    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes) + 16 + 16 * n;
 }
 
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {
@@ -1069,8 +1078,9 @@ static fmx_status ensure_ws(fmx_index *ix, uint64_t n) {
     const uint64_t want = std::max<uint64_t>(need, 1 << 16);
     if (hipMalloc(&ix->d_ws, want) != hipSuccess) return FMX_E_DEVICE;
     // zeroed on the index's own (non-blocking) stream, which the host-API
-    // launches use: a plain hipMemset runs on the null stream, unordered
-    // with it, and a grouped launch's key counters must start at zero
+    // launches use (a plain hipMemset runs on the null stream, unordered with
+    // it); only the persistent-grid A/B variant's tile counter needs it (a
+    // grouped launch zeroes its own key counters)
     if (hipMemsetAsync(ix->d_ws, 0, want, ix->stream) != hipSuccess) return FMX_E_DEVICE;
     if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
     ix->ws_bytes = want;

@@ -13,6 +13,12 @@
 
 #include "../../include/fmx.h"
 
+// A kernel's dynamic LDS (a macro: the host emulation under tests/simt
+// supplies its own buffer per workgroup).
+#ifndef FMX_DYN_LDS
+#define FMX_DYN_LDS(name) extern __shared__ uint8_t name[]
+#endif
+
 namespace fmx {
 
 constexpr int kMaxSigma = 64;  // Block6 indexes at most 2^6 symbols (blocks/block6.rs:15)
@@ -92,6 +98,7 @@ constexpr uint64_t kKmerLdsMax = 4096;    // k-mer count tables up to this size 
 constexpr uint32_t kStatusEmpty = 1u;
 constexpr uint32_t kStatusSymbol = 2u;
 constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
+constexpr uint32_t kStatusGroup = 16u;  // a grouped launch's sorted position out of range (never expected)
 
 // One bracketed launch of a timer: events a -> b; own_a / own_b say whether
 // this entry returns the event to the pool when read (a split launch's
@@ -146,10 +153,11 @@ struct fmx_index {
     uint64_t status_clock = 0;
     bool status_pressure = false;  // most words assigned: launches record completion events
     bool search_persistent = false;  // FMX_SEARCH_PERSISTENT=1: k_search on a resident-sized grid (A/B)
-    // grouped launches (fmx::kWsHeader), opt-in: launches of at least
-    // grouped_min patterns (FMX_GROUPED_MIN; FMX_GROUPED=1 every launch; the
-    // default never) on the faithful index; the key = the last gkey_len
-    // symbols, digits over the gkey_base symbols that occur in the text
+    // grouped launches (fmx::kWsHeader): launches of at least grouped_min
+    // patterns on the faithful index — by default 131,072 when the key spans
+    // at least 5 symbols (finish_load), FMX_GROUPED_MIN sets it, FMX_GROUPED=1
+    // groups every launch that can be, FMX_GROUPED=0 none; the key = the last
+    // gkey_len symbols, digits over the gkey_base symbols that occur in the text
     uint64_t grouped_min = 0;
     uint32_t gkey_len = 0, gkey_base = 0;
     uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
@@ -214,11 +222,13 @@ struct LocateGroup {
     uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
     uint32_t n;
     // Grouped launch (kWsHeader below): the group's key counters (batch 0's
-    // workspace, zero between launches: k_group_tiles re-zeroes them), the
-    // key's symbol count and digit base, the bits per packed symbol, and the
-    // first key/place workgroup of each batch; gcount null = launch order
+    // workspace, zeroed on the launch's stream before its first kernel), the
+    // key's symbol count and digit base, the bits per packed symbol, the
+    // launch's pattern count, and the first key/place workgroup of each
+    // batch; gcount null = launch order
     uint32_t *gcount;
     uint32_t gkey_len, gkey_base, gbits;
+    uint64_t gtotal;
     uint32_t chunk_begin[kMaxGroup];
     // FMX_SEARCH_PERSISTENT=1 (A/B): k_search runs a resident-sized grid whose
     // workgroups take tiles from this counter (batch 0's workspace header,
@@ -246,8 +256,9 @@ constexpr uint64_t kFoldTiles = 2048;
 // locate_rec_bytes):
 //   [256 B header][kGroupCounterRoom u32 key counters][tile counts: G][tile
 //   offsets: G][search records: n x R][its share of the sorted order: n x 16 B]
-// The counters sit at a fixed offset so that every launch on a workspace
-// finds them zero whatever its n.
+// The counters sit at a fixed offset in batch 0's workspace; every grouped
+// launch zeroes them on its stream first (16 KB, a few microseconds), so no
+// launch depends on how an earlier one on the workspace ended.
 #ifndef FMX_GROUP_KEY_BITS
 #define FMX_GROUP_KEY_BITS 12  // (build option, A/B: 14 = 16,384 bins, C2 keys on 7 symbols)
 #endif

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void k_count(const QueryArgs a, const uint8_t 
                                                const uint64_t *__restrict__ offs, uint64_t npat,
                                                uint32_t flags, P *__restrict__ out_cnt, uint32_t stage_bytes) {
     __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    FMX_DYN_LDS(s_pat);  // stage_bytes, then the k-mer table (dynamic)
     stage_tables(a, s, s_pat + stage_bytes);
     __syncthreads();
     const bool rev = (flags & FMX_PATTERN_REVERSED) != 0;
@@ -369,7 +369,7 @@ template <typename P, int N, int VB, int REC, int VAR>
 __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search(const QueryArgs a, const LocateGroup grp,
                                                              uint32_t stage_bytes) {
     __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    FMX_DYN_LDS(s_pat);  // stage_bytes, then the k-mer table (dynamic)
     __shared__ uint64_t s_scan[4];
     stage_tables(a, s, s_pat + stage_bytes);
     search_tile<P, N, VB, REC, VAR>(a, grp, s, s_pat, s_scan, stage_bytes, blockIdx.x);
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
                                                                                       uint32_t stage_bytes,
                                                                                       uint32_t tiles) {
     __shared__ Tables<P> s;
-    extern __shared__ uint8_t s_pat[];  // stage_bytes, then the k-mer table (dynamic)
+    FMX_DYN_LDS(s_pat);  // stage_bytes, then the k-mer table (dynamic)
     __shared__ uint64_t s_scan[4];
     __shared__ uint32_t s_tile;
     stage_tables(a, s, s_pat + stage_bytes);
@@ -412,10 +412,11 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
 using U4 = uint32_t __attribute__((ext_vector_type(4)));
 
 // A batch's share of the launch's sorted order ({symbols: 96 bits, pattern
-// id} per position), after its search records.
+// id} per position), after its search records, 16-B aligned (24-B records
+// of u64 positions leave an odd count 8-B aligned).
 __device__ __forceinline__ U4 *group_sorted(const LocateBatch &B, uint32_t rec_bytes) {
     const uint64_t n = B.npat, G = (n + 255) / 256;
-    return reinterpret_cast<U4 *>(reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + n * rec_bytes);
+    return reinterpret_cast<U4 *>(reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + ((n * rec_bytes + 15) & ~15ull));
 }
 
 // This workgroup's batch of a key launch (workgroup-uniform, binary search).
@@ -576,6 +577,10 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
             const uint64_t i = first + p * T + t;
             if (i >= n) continue;
             const uint64_t sp = (uint64_t)hist[key_r[p]] + rank_r[p];
+            if (sp >= grp.gtotal) {  // (counters not zero at entry: never write outside the sorted order)
+                atomicOr(a.status, kStatusGroup);
+                continue;
+            }
             const uint32_t js = lds_upper(s_first, grp.n, sp);
             s_sorted[js][sp - s_first[js]] = rec_r[p];
         }
@@ -622,7 +627,7 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     __shared__ GroupBatch<P> sb[kMaxGroup];
     __shared__ uint64_t s_first[kMaxGroup];   // the launch's patterns before batch j
     __shared__ uint32_t s_vfirst[kMaxGroup];  // batch j's first pattern id (tile_begin * 256)
-    extern __shared__ uint8_t s_pat[];  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
+    FMX_DYN_LDS(s_pat);  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
     stage_tables(a, s, s_pat + 256 * K * cap);
     for (uint32_t j = threadIdx.x; j < grp.n; j += 256) {
         const LocateBatch &B = grp.b[j];

@@ -23,7 +23,6 @@
 // make each LF step cost one record read per rank query — one for both when
 // lo and hi share a block.
 #include <cstring>
-#include <rocprim/rocprim.hpp>
 
 #include "fmx_kernels.hpp"
 
@@ -87,10 +86,9 @@ __global__ __launch_bounds__(256) void k_group_scan(uint32_t *cnt) {
 }
 
 // 4. Each tile's count (k_emit's tile offsets) and each pattern's count (the
-// optional counts output, in order here), and the key counters zeroed again
-// for the workspace's next grouped launch.
+// optional counts output, in order here).
 template <typename P>
-__global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp, uint32_t tiles) {
+__global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp) {
     __shared__ uint64_t s_w[4];
     const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
     const LocateBatch &B = grp.b[jb];
@@ -104,8 +102,6 @@ __global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp, uint
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = cnt;
-    for (uint64_t x = (uint64_t)vt * 256u + threadIdx.x; x < kGroupBins; x += (uint64_t)tiles * 256u)
-        grp.gcount[x] = 0;
     __syncthreads();
     if (threadIdx.x == 0) B.tiles[g] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
@@ -252,6 +248,11 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     grp.gkey_len = ix->gkey_len;
     grp.gkey_base = ix->gkey_base;
     grp.gbits = bits;
+    grp.gtotal = total;
+    // the key counters start at zero whatever an earlier launch on this
+    // workspace did: ordered before the count pass on the stream
+    hipError_t e = hipMemsetAsync(grp.gcount, 0, 4ull * kGroupBins, stream);
+    if (e != hipSuccess) return e;
     uint32_t chunks = 0;
     for (uint32_t j = 0; j < grp.n; ++j) {
         grp.chunk_begin[j] = chunks;
@@ -269,7 +270,7 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
         hipLaunchKernelGGL((k_group_key<8, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     else
         hipLaunchKernelGGL((k_group_key<25, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);
     if (maxm <= 21)
@@ -286,9 +287,9 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
         hipSuccess)
         return e;
     if (p4)
-        hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(tiles), dim3(256), 0, stream, grp, tiles);
+        hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(tiles), dim3(256), 0, stream, grp);
     else
-        hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(tiles), dim3(256), 0, stream, grp, tiles);
+        hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(tiles), dim3(256), 0, stream, grp);
     return hipGetLastError();
 }
 

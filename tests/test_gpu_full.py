@@ -3,8 +3,9 @@ is built on the GPU from a seeded synthetic text, copied to the host, and the
 oracle (oracle/fmx_oracle.c, the C restatement of the reference's query path)
 answers the same patterns on the same blob bytes.  Every count and every
 location (suffix-array-row order) of the GPU must equal the oracle's, under
-the faithful index (FMX_OPT_DEFAULT) and every derived structure
-(FMX_OPT_DERIVED).  Sizes are the configs' own: 1 Gbp / 1 G residues / 3 Gbp
+the default index (FMX_OPT_DEFAULT: interleaved records) in launch order and
+with the launch grouped (FMX_GROUPED=1), and on the blob as laid out
+(FMX_OCC_BLOB).  Sizes are the configs' own: 1 Gbp / 1 G residues / 3 Gbp
 texts; 100,000 patterns each (C5: a 100,000-pattern subset of its 1 M)."""
 import os
 
@@ -68,14 +69,25 @@ def run_config(pkg, O, n, alphabet, symbols, pos, planes, vec, m, npat, seed, ex
              + ", ".join(f"{bytes(pats[int(offsets[i]):int(offsets[i + 1])])!r} x{int(cnts[i])}" for i in top)
              + f"; zero counts: {int((cnts[:npat] == 0).sum())}")
     starts_h = starts.cpu().numpy()
-    for options in (pkg._native.FMX_OPT_DEFAULT, pkg._native.FMX_OPT_DERIVED):
-        ix = pkg.FmIndex.load(blob, position, block, table, options=options)
+    runs = ((pkg._native.FMX_OPT_DEFAULT, None), (pkg._native.FMX_OPT_DEFAULT, "1"), (pkg._native.FMX_OCC_BLOB, None))
+    for options, grouped in runs:
+        saved = os.environ.get("FMX_GROUPED")
+        if grouped is not None:
+            os.environ["FMX_GROUPED"] = grouped  # (read at load)
+        try:
+            ix = pkg.FmIndex.load(blob, position, block, table, options=options)
+        finally:
+            if grouped is not None:
+                if saved is None:
+                    del os.environ["FMX_GROUPED"]
+                else:
+                    os.environ["FMX_GROUPED"] = saved
         goff, glocs = ix.locate_batch((pats, offsets))
-        assert np.array_equal(goff, ooff), f"offsets differ, options {options}"
-        assert np.array_equal(glocs, olocs), f"locations differ, options {options}"
+        assert np.array_equal(goff, ooff), f"offsets differ, options {options} grouped {grouped}"
+        assert np.array_equal(glocs, olocs), f"locations differ, options {options} grouped {grouped}"
         cnt = ix.count_batch((pats, offsets))
         assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff))
-        progress(f"options {options}: bit-exact")
+        progress(f"options {options} grouped {grouped}: bit-exact")
         ix.close()
     # the size-independent property: every cut pattern finds its own start
     own = np.zeros(npat, dtype=bool)
