@@ -127,7 +127,8 @@ def parse():
     ap.add_argument("--derived", action="store_true", help="also run the derived-index leg (~147 GB at C2)")
     ap.add_argument("--derived-options", type=int, default=DERIVED)
     ap.add_argument("--no-derived", action="store_true", help=argparse.SUPPRESS)  # (the default now)
-    ap.add_argument("--min-seconds", type=float, default=0.2, help="minimum timed region (passes repeated)")
+    ap.add_argument("--min-seconds", type=float, default=2.0,
+                    help="minimum timed region (passes repeated; >= 2 s so that an outside sampler sees the GPU busy)")
     ap.add_argument("--event-every", type=int, default=5,
                     help="bracket every k-th launch of the timed region with HIP events")
     ap.add_argument("--kernel-launches", type=int, default=8,
@@ -141,6 +142,10 @@ def parse():
     ap.add_argument("--no-fixed-len", action="store_true",
                     help="A/B: do not pass FMX_HINT_FIXED_LEN (the kernels read each tile's offsets first)")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-single-batch", action="store_true",
+                    help="skip the single_batch leg (one 100k batch per fmx_locate_batch_async call)")
+    ap.add_argument("--single-batch-only", action="store_true",
+                    help="run only the headline setup and the single_batch leg (no other legs)")
     ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
     ap.add_argument("--batches", type=int, default=32,
                     help="distinct batches cycled (weak-scaling configs; at least one launch group per stream)")
@@ -627,16 +632,19 @@ def main():
     torch.cuda.synchronize()
 
     jg = None
-    if strong:
-        # size every batch's location slot from the warm-up (the same job runs
-        # in the timed region), exchange the sizes once, and point the kernels'
-        # outputs straight into the gather slabs
+    if strong or dist_on:
+        # size every batch's location slot from the warm-up (the same batches
+        # run in the timed region), exchange the sizes once, and point the
+        # kernels' outputs straight into the gather slabs: a sharded job's
+        # (c3/c5), or every rank's own batches (c2 weak scaling), so that the
+        # results are concatenated on every rank inside the timed step
         for q in range(max(args.warmup, w.n_groups)):
             w.launch(q % w.n_groups)
         torch.cuda.synchronize()
         needs = w.check_capacity()
         all_needs = D.all_gather_ints(needs, device=dev)
-        jg = D.JobGather(plan.sizes(), all_needs, GR, rank, pdt_t, dev)
+        sizes = plan.sizes() if strong else np.full((world, len(w.batches)), B, dtype=np.int64)
+        jg = D.JobGather(sizes, all_needs, GR, rank, pdt_t, dev)
         w.rebind([(jg.counts_slot(k), jg.locs_slot(k)) for k in range(len(w.batches))])
 
     # ---- timed region: compute ----------------------------------------------
@@ -663,9 +671,12 @@ def main():
                            "patterns_per_rank": [e - s for s, e in plan.spans],
                            "batch_patterns_min": int(plan.sizes().min()), "batch_patterns_max": plan.max_batch()},
                   "needs_stable": needs_after == needs}
-    if dist_on and strong:
+    if dist_on:
         # the same passes with each launch group's results all-gathered (one
         # collective) on a communication stream while the next launch computes
+        # (strong: the job's slab of that group; weak: every rank's batches of
+        # that group) — the north star's "single RCCL all-gather over xGMI to
+        # concatenate results", inside the timed step
         comm = torch.cuda.Stream(device=dev)
         works, gathered = [], {}
 
@@ -695,48 +706,33 @@ def main():
                                            args.event_every, on_launch=on_launch, pre_launch=pre_launch,
                                            drain=drain)
         e2 = D.max_over_ranks(e2, device=dev)
-        value = total * p2 / e2
+        pt2 = torch.tensor([pats2 * p2], dtype=torch.int64, device=dev)
+        dist.all_reduce(pt2)
+        value = int(pt2.item()) / e2
+        if gather is None:
+            gather = {}
         gather.update({"inside_timed_step": True, "value_compute_only": value_compute,
                        "collectives_per_launch": 1,
                        "bytes_gathered_per_pass": jg.bytes_per_pass(),
                        "result_bytes_per_pass": jg.result_bytes(),
                        "gathered_over_result": jg.bytes_per_pass() / max(jg.result_bytes(), 1)})
-    elif dist_on:
-        # weak scaling: every batch's counts and locations, after the timed
-        # region, in one exactly sized gather
-        needs = w.needs()
-        all_needs = D.all_gather_ints(needs, device=dev)
-        sizes = np.full((world, len(w.batches)), B, dtype=np.int64)
-        jw = D.JobGather(sizes, all_needs, len(w.batches), rank, pdt_t, dev)
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        for k, bt in enumerate(w.batches):
-            jw.counts_slot(k).copy_(bt["cnt"][:bt["n"]], non_blocking=True)
-            jw.locs_slot(k).copy_(bt["locs"][:needs[k]], non_blocking=True)
-        jw.gather_all()
-        offs_all, locs_all = jw.assemble()
-        torch.cuda.synchronize()
-        gather = {"inside_timed_step": False, "gather_ms": (time.perf_counter() - tg) * 1e3,
-                  "bytes_gathered": jw.bytes_per_pass(), "result_bytes": jw.result_bytes(),
-                  "batches": len(w.batches)}
-        # this rank's batches came back intact
-        p0 = rank * len(w.batches) * B
-        mine_c = torch.cat([bt["cnt"][:bt["n"]] for bt in w.batches]).to(torch.int64)
-        l0 = int(all_needs[:rank].sum())
-        mine_l = torch.cat([bt["locs"][:needs[k]] for k, bt in enumerate(w.batches)])
-        gather["roundtrip_ok"] = bool(torch.equal(torch.diff(offs_all[p0:p0 + mine_c.numel() + 1]), mine_c) and
-                                      torch.equal(locs_all[l0:l0 + mine_l.numel()], mine_l))
-    if strong:
+    if jg is not None:
         # the job's flat (offsets, locations) on the device; this rank's part
         # must equal what its own launches wrote
         offs_job, locs_job = jg.assemble()
-        s0, e0 = plan.spans[rank]
+        s0, e0 = plan.spans[rank] if strong else (rank * len(w.batches) * B, (rank + 1) * len(w.batches) * B)
         mine = torch.cat([bt["cnt"] for bt in w.batches]).to(torch.int64)
+        if gather is None:
+            gather = {}
         gather["assembled_patterns"] = int(offs_job.numel() - 1)
         gather["assembled_locations"] = int(locs_job.numel())
-        gather["assembly_ok"] = bool(offs_job.numel() == total + 1 and
+        gather["assembly_ok"] = bool(offs_job.numel() == int(jg.sizes.sum()) + 1 and
                                      int(offs_job[-1].item()) == locs_job.numel() == int(jg.needs.sum()) and
                                      torch.equal(torch.diff(offs_job[s0:e0 + 1]), mine))
+
+    # what `value` was timed over (N > 1: the passes with the in-step gathers)
+    region_s, passes_timed = (e2, p2) if dist_on else (elapsed, passes)
+    steps_timed = per_pass * passes_timed
 
     # ---- roofline --------------------------------------------------------------
     # Algorithmic bytes: per pattern m + 2P (k-mer seed) +
@@ -764,7 +760,9 @@ def main():
     tr = traffic_of(args.traffic_json, key)
     roof = {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-        "traffic": tr["fabric_bytes_per_launch"] if tr else None,
+        # memory-side bytes per launch (reads from the request split + writes), rocprofv3 PMC passes of this
+        # build under this profile key (scripts/gpu.sh pmc + scripts/traffic.py)
+        "traffic": tr.get("traffic_bytes_per_launch", tr.get("fabric_bytes_per_launch")) if tr else None,
         "achieved_basis": "per-step cost: the reference algorithm's bytes per pattern (SURVEY.md 8(d), "
                           "alg_bytes_per_pattern) x the timed region's patterns/s per GPU",
         "alg_bytes_per_pattern": alg_per_pattern,
@@ -784,15 +782,24 @@ def main():
     }
     if tr:
         req = tr.get("fabric_requests_per_launch")
-        tpp = tr["fabric_bytes_per_launch"] / tr.get("patterns_per_launch", ppl or 1)
+        tppl = tr.get("patterns_per_launch", ppl or 1)
+        tpp = roof["traffic"] / tppl
         roof.update({
-            "traffic_what": "memory-side (fabric) read bytes per launch: TCC_EA0_RDREQ requests x their size; on "
-                            "gfx950 these include Infinity Cache hits (MI355X_MICROARCH.md, HBM section), so "
-                            "they bound HBM bytes from above",
+            "traffic_what": "memory-side bytes per launch of the headline's launch shape (a launch = "
+                            "patterns_per_launch patterns; every kernel of the launch): reads = TCC_EA0_RDREQ "
+                            "requests x their size (32/64/128 B), writes = WRITE_SIZE; on gfx950 these include "
+                            "Infinity Cache hits (MI355X_MICROARCH.md, HBM section), so they bound HBM bytes from "
+                            "above",
             "traffic_source": f"{os.path.relpath(args.traffic_json, ROOT)} [{key}] ({tr.get('source')})",
-            "fabric_bytes_per_pattern": tpp,
-            "fabric_frac_effective": tpp * per_gpu / 1e9 / HBM_PEAK_GBS,
+            "traffic_patterns_per_launch": tppl,
+            "traffic_bytes_per_pattern": tpp,
+            "traffic_over_alg": tpp / alg_per_pattern,
+            "fabric_read_bytes_per_pattern": tr["fabric_bytes_per_launch"] / tppl,
+            "traffic_frac_effective": tpp * per_gpu / 1e9 / HBM_PEAK_GBS,
         })
+        if tr.get("search_kernel"):
+            roof["kernel"]["traffic_bytes_per_pattern"] = tr["search_kernel"].get("traffic_bytes_per_pattern")
+            roof["kernel"]["fabric_requests_per_pattern"] = tr["search_kernel"].get("fabric_requests_per_pattern")
         if req:
             rpp = req / tr.get("patterns_per_launch", ppl or 1)
             roof.update({"fabric_requests_per_pattern": rpp, "fabric_grequests_per_s": rpp * per_gpu / 1e9,
@@ -809,12 +816,16 @@ def main():
         "ranks": world,
         "rccl_world_size": world if (dist_on and backend == "nccl") else None,
         "backend": backend if dist_on else None,
-        "steps": steps,
+        "steps": steps_timed,
+        "steps_requested": args.steps or None,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / (per_pass * passes) * 1e3,
-        "timed_passes": passes,
+        "ms_per_step": region_s / steps_timed * 1e3,
+        "timed_passes": passes_timed,
         "batches_per_pass": per_pass,
-        "timed_region_s": elapsed,
+        "timed_region_s": region_s,
+        "steps_what": "batches (steps) timed: whole launches of up to batches_per_launch batches, passes repeated "
+                      "until the region lasts >= --min-seconds; the requested --steps is rounded up to whole "
+                      "launches per pass" + ("; N > 1: the passes with the in-step all-gathers" if dist_on else ""),
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
@@ -870,6 +881,14 @@ def main():
         if not result["parity"]["bit_exact_vs_cpu"]:
             log("PARITY FAILURE: the assembled job differs from the CPU oracle")
         del orc
+
+    # ---- one batch per call (the config's own batch, N = 1) ------------------
+    if rank == 0 and world == 1 and not strong and not args.no_single_batch:
+        result["single_batch"] = single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, args.seed,
+                                                  min(args.min_seconds, 1.0), pdt_t, P)
+    if args.single_batch_only:
+        args.no_blob_layout = args.no_cpu = True
+        args.derived = False
 
     # ---- the blob's own layout (options 0, N = 1) -----------------------------
     # the GPU's answers for the CPU leg to check (up to 32 batches, host copies)
@@ -980,6 +999,74 @@ def main():
     ix.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, seed, min_seconds, pdt_t, P):
+    """BASELINE configs[1] as a caller of the reference's per-batch loop gets
+    it (bench/src/locate/sview_memory.rs:32: one batch of 100,000 patterns per
+    call): one fmx_locate_batch_async call per batch on one stream, calls back
+    to back (each waits only for the stream), 32 distinct batches cycled for
+    >= min_seconds — in launch order (FMX_GROUPED=0) and grouped
+    (FMX_GROUPED=1: the batch dealt out by its last symbols on its own), each
+    on an index of its own (the policy is read at load)."""
+    out = {"what": "one 100k-pattern batch per fmx_locate_batch_async call, one stream, calls back to back; "
+                   "the headline instead runs 256 batches per grouped launch (fmx_locate_group_async) on 2 streams"}
+    stage_kb = min(56, -(-256 * m // 1024))
+    for mode, name in (("0", "launch_order"), ("1", "grouped")):
+        saved = os.environ.get("FMX_GROUPED")
+        os.environ["FMX_GROUPED"] = mode
+        try:
+            ixs, _ = load(FAITHFUL)
+        finally:
+            if saved is None:
+                del os.environ["FMX_GROUPED"]
+            else:
+                os.environ["FMX_GROUPED"] = saved
+        stream = torch.cuda.Stream(device=dev)
+        bats = []
+        for bi in range(32):
+            pg = torch.Generator(device=dev)
+            pg.manual_seed(seed * 1000 + 50021 * bi + 13)
+            st = torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg)
+            cap = B + B // 8 + 4096
+            bats.append(dict(starts=st, pat=cut_patterns(torch, d_text, st, m),
+                             off=torch.arange(B + 1, device=dev, dtype=torch.int64) * m,
+                             loff=torch.zeros(B + 1, dtype=torch.int64, device=dev),
+                             need=torch.zeros(1, dtype=torch.int64, device=dev),
+                             locs=torch.zeros(cap, dtype=pdt_t, device=dev), cap=cap,
+                             ws=torch.zeros(ixs.locate_workspace_size(B), dtype=torch.uint8, device=dev),
+                             cnt=torch.zeros(B, dtype=pdt_t, device=dev)))
+        torch.cuda.synchronize()
+
+        def call(b):
+            ixs.locate_batch_async(b["pat"].data_ptr(), b["off"].data_ptr(), B, b["loff"].data_ptr(),
+                                   b["locs"].data_ptr(), b["cap"], b["need"].data_ptr(), b["ws"].data_ptr(),
+                                   b["ws"].numel(), d_counts=b["cnt"].data_ptr(), stream=stream.cuda_stream,
+                                   stage_kb=stage_kb, fixed_len=fixed)
+
+        for b in bats:
+            call(b)
+        ixs.sync(stream.cuda_stream)
+        calls, t0 = 0, time.perf_counter()
+        while True:
+            for b in bats:
+                call(b)
+            calls += len(bats)
+            if time.perf_counter() - t0 >= min_seconds:
+                break
+        ixs.sync(stream.cuda_stream)
+        el = time.perf_counter() - t0
+        need = [int(b["need"].item()) for b in bats]
+        if any(nd > b["cap"] for nd, b in zip(need, bats)):
+            raise SystemExit("single_batch: location buffer too small")
+        w1 = type("W", (), {})()
+        w1.batches = [dict(n=B, loff=b["loff"], locs=b["locs"], starts=b["starts"]) for b in bats[:4]]
+        out[name] = {"value": calls * B / el, "unit": "patterns/s", "us_per_batch": el / calls * 1e6,
+                     "calls": calls, "self_location_check": self_location(w1, P)}
+        ixs.release_stream(stream.cuda_stream)
+        del bats
+        ixs.close()
+    return out
 
 
 def arrange(torch, w, B, m, GR, dev, presorted, key_symbols=14):

@@ -9,6 +9,8 @@
 #   trace    rocprofv3 --kernel-trace --stats on bench.py --streams 1 and on the default command
 #   pmc      rocprofv3 PMC passes (FETCH/WRITE size, memory-side requests) on bench.py --streams 1
 #   configs  bench.py --config c1 / c3 / c4 / c5
+#   cli      bench_cli.py: generate, build, locate warm / cold / O_DIRECT (the README workload)
+#   gloo2    bench.py --gpus 2 over gloo on the one GPU (the multi-rank path: in-step gathers)
 # Every step has its own time limit; the first failing step ends the run.
 # Output: gpurun_out/TAG/*.
 set -o pipefail
@@ -34,21 +36,34 @@ for step in "$@"; do
             run bench_default 400 python -u bench.py || exit 1
             run bench_driver 400 python -u bench.py --steps 20 --warmup 5 || exit 1 ;;
         single) run bench_single 300 python -u bench.py --single-batch-only || exit 1 ;;
+        gloo2) FMX_BENCH_BACKEND=gloo run bench_gloo2 600 python -u bench.py --gpus 2 --no-cpu || exit 1 ;;
         trace)
-            run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run -- \
-                python -u bench.py --streams 1 --no-cpu || exit 1
-            run trace_default 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace2" -o run -- \
-                python -u bench.py --no-cpu || exit 1 ;;
+            run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run --output-format csv -- \
+                python3 -u bench.py --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1
+            run trace_default 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace2" -o run --output-format csv -- \
+                python3 -u bench.py --no-cpu || exit 1 ;;
         pmc)
-            for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_REQ_sum TCC_HIT_sum"; do
-                nm=$(echo "$ctr" | tr ' ' '_')
-                run "pmc_$nm" 300 rocprofv3 --pmc $ctr -d "$OUT/pmc_$nm" -o run -- \
-                    python -u bench.py --streams 1 --no-cpu || exit 1
-            done ;;
+            P="--streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+            run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \
+                --output-format csv -- python3 -u bench.py $P || exit 1
+            run pmc_ea 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+                --kernel-trace -d "$OUT/pmc_ea" -o run --output-format csv -- python3 -u bench.py $P || exit 1
+            run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run \
+                --output-format csv -- python3 -u bench.py $P || exit 1
+            run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$OUT/pmc_tcc" -o run \
+                --output-format csv -- python3 -u bench.py $P || exit 1 ;;
         configs)
             for c in c1 c3 c4 c5; do
                 run "bench_$c" 600 python -u bench.py --config $c || exit 1
             done ;;
+        cli)  # the reference bench's workflow end to end at the README workload, warm and cold
+            D=$PWD/.fmx_cli; rm -rf "$D"; mkdir -p "$D"; CLI="python sview-fmindex_amd/bench_cli.py"
+            run cli_generate 420 bash -c "$CLI generate-text -d $D -t 1000000000 -s 7 && \
+                $CLI generate-pattern -d $D -p 20 -n 100000 -s 7 && $CLI build -d $D -a all -s 2 -k 3" || exit 1
+            run cli_locate 900 bash -c "$CLI locate -d $D -a sview-memory && $CLI locate -d $D -a sview-mmap && \
+                $CLI locate -d $D -a sview-memory --drop-caches && $CLI locate -d $D -a sview-mmap --drop-caches && \
+                $CLI locate -d $D -a sview-mmap --drop-caches --direct && md5sum $D/*-results.txt" || exit 1
+            rm -rf "$D" ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

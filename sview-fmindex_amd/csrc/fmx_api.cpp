@@ -481,6 +481,8 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (const char *e = getenv("FMX_GROUPED_XCD")) ix->grouped_xcd = e[0] == '1';
     ix->grouped_pair = 0;
     if (const char *e = getenv("FMX_GROUPED_PAIR")) ix->grouped_pair = e[0] == '1';
+    ix->grouped_raw = false;
+    if (const char *e = getenv("FMX_GROUPED_RAW")) ix->grouped_raw = e[0] == '1';
     if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
         // the largest K with S^K * 2P <= budget, deeper than the blob's k;
         // budget: FMX_DEEP_LUT_MB, else 160 GiB capped at half the free HBM

@@ -162,6 +162,7 @@ struct fmx_index {
     uint32_t gkey_len = 0, gkey_base = 0;
     uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
     uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
+    bool grouped_raw = false;  // FMX_GROUPED_RAW=1: id-only sorted records even for patterns that pack (A/B)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -228,6 +229,7 @@ struct LocateGroup {
     // batch; gcount null = launch order
     uint32_t *gcount;
     uint32_t gkey_len, gkey_base, gbits;
+    uint32_t graw;  // 1: the sorted records hold pattern ids alone (patterns too long to pack)
     uint64_t gtotal;
     uint32_t chunk_begin[kMaxGroup];
     // FMX_SEARCH_PERSISTENT=1 (A/B): k_search runs a resident-sized grid whose

@@ -462,7 +462,12 @@ __device__ __forceinline__ uint32_t lds_upper(const T *tab, uint32_t n, K x) {
 //     (tile_begin * 256 + index), is written at its sorted position (chunk
 //     base + rank) — the sorted order is held by the batches one after
 //     another.
-template <int W, bool PLACE>
+//   RAW (grp.graw: patterns too long to pack, e.g. C5's 150 bp): only the W
+//     words holding the key's symbols are read (the pattern's last gkey_len
+//     symbols: its last bytes, or its first for reversed input), and the
+//     record carries the pattern id alone — k_search_grouped reads the
+//     pattern's bytes itself.
+template <int W, bool PLACE, bool RAW = false>
 __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
     constexpr uint32_t T = 1024, PPT = kGroupChunkTiles * 256 / T;  // patterns per thread
     __shared__ uint8_t s_enc[256];
@@ -501,15 +506,19 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     for (uint32_t p0 = 0; p0 < PPT; p0 += G) {
     uint32_t x[G][W], lead[G];
     uint64_t chk[G];
+    // the bytes read: the whole pattern, or (RAW) its key's: the last kl
+    // input bytes, or the first kl of a reversed one
+    const uint32_t kl = L < m ? L : m, span = RAW ? kl : m;
+    const uint32_t skip = RAW && !rev ? m - kl : 0u;  // input bytes before the span
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
         const uint64_t i = first + (p0 + g) * T + t;
-        const uint64_t beg = i * m, a0 = beg & ~3ull;
+        const uint64_t beg = i * m + skip, a0 = beg & ~3ull;
         lead[g] = (uint32_t)(beg - a0);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(B.bytes + a0);
         const bool ok = i < n;
 #pragma unroll
-        for (uint32_t q = 0; q < W; ++q) x[g][q] = ok && 4 * q < lead[g] + m ? src[q] : 0u;
+        for (uint32_t q = 0; q < W; ++q) x[g][q] = ok && 4 * q < lead[g] + span ? src[q] : 0u;
         chk[g] = ok && !PLACE ? B.offs[i + 1] : 0;
     }
 #pragma unroll
@@ -523,13 +532,14 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
         uint32_t key = 0;
 #pragma unroll
         for (uint32_t b = 0; b < 4 * W; ++b) {
-            const uint32_t pos = b - lead[g];  // input byte index (wraps below 0: skipped)
-            if (pos >= m) continue;
+            const uint32_t sp = b - lead[g];  // byte of the span (wraps below 0: skipped)
+            if (sp >= span) continue;
+            const uint32_t pos = sp + skip;  // input byte index
             const uint32_t j = rev ? m - 1 - pos : pos;  // pattern position
             uint32_t cj = s_enc[(x[g][b >> 2] >> (8 * (b & 3))) & 0xffu];
             const uint32_t back = m - 1 - j;  // 0 = the last symbol
             if (back < L) key += (cj < (uint32_t)kMaxSigma ? s_dig[cj] : 0u) * s_pw[L - 1 - back];
-            if constexpr (PLACE) {
+            if constexpr (PLACE && !RAW) {
                 cj = cj < sym_max ? cj : sym_max;
                 const uint32_t at = j * bits;
                 if (at < 64) {
@@ -593,7 +603,8 @@ template <typename P>
 struct GroupBatch {
     SearchRec<P> *recs;
     const U4 *sorted;
-    uint32_t stride;
+    const uint8_t *bytes;  // (raw records: the patterns, read by the search)
+    uint32_t stride, rev;
 };
 
 // 3. Search the launch's patterns in key order: workgroup b takes sorted
@@ -634,7 +645,9 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         const uint64_t G = (B.npat + 255) / 256;
         sb[j].recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
         sb[j].sorted = group_sorted(B, sizeof(SearchRec<P>));
+        sb[j].bytes = B.bytes;
         sb[j].stride = B.stride;
+        sb[j].rev = B.rev;
         s_first[j] = B.first;
         s_vfirst[j] = grp.tile_begin[j] * 256u;
     }
@@ -671,7 +684,13 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         pj[q] = jb;
         pi[q] = (uint64_t)(v - s_vfirst[jb]);
         pv[q].m = sb[jb].stride;
-        grouped_unpack<P>(e, sb[jb].stride, grp.gbits, dst);
+        if (grp.graw) {  // the pattern's own bytes (input order), encoded on each access
+            pv[q].raw = sb[jb].bytes + pi[q] * sb[jb].stride;
+            pv[q].rev = sb[jb].rev != 0;
+            pv[q].sym = nullptr;
+        } else {
+            grouped_unpack<P>(e, sb[jb].stride, grp.gbits, dst);
+        }
     }
     P lo_r[K], hi_r[K], rloc[K];
     uint64_t mask[K];

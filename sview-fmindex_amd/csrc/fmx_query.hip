@@ -242,12 +242,13 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
 // A grouped launch's search (kWsHeader): key counts, their scan, the sorted
 // order, the search in key order, tile counts.
 static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
-                                        uint64_t total, uint32_t sb, uint32_t bits, hipStream_t stream) {
+                                        uint64_t total, uint32_t sb, uint32_t bits, bool raw, hipStream_t stream) {
     const Disp d = dispatch(ix);
     grp.gcount = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader + 256);
     grp.gkey_len = ix->gkey_len;
     grp.gkey_base = ix->gkey_base;
     grp.gbits = bits;
+    grp.graw = raw ? 1u : 0u;
     grp.gtotal = total;
     // the key counters start at zero whatever an earlier launch on this
     // workspace did: ordered before the count pass on the stream
@@ -263,8 +264,11 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     // the key passes hold each pattern in W registers
     uint32_t maxm = 1;
     for (uint32_t j = 0; j < grp.n; ++j) maxm = std::max<uint32_t>(maxm, grp.b[j].stride);
-    // (W = 6 words hold patterns up to 21 bytes at any alignment, 8 up to 29, 25 up to 97)
-    if (maxm <= 21)
+    // (W = 6 words hold patterns up to 21 bytes at any alignment, 8 up to 29, 25 up to 97; raw: the key's
+    // gkey_len <= 16 bytes in 5)
+    if (raw)
+        hipLaunchKernelGGL((k_group_key<5, false, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    else if (maxm <= 21)
         hipLaunchKernelGGL((k_group_key<6, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     else if (maxm <= 29)
         hipLaunchKernelGGL((k_group_key<8, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
@@ -273,7 +277,9 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);
-    if (maxm <= 21)
+    if (raw)
+        hipLaunchKernelGGL((k_group_key<5, true, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    else if (maxm <= 21)
         hipLaunchKernelGGL((k_group_key<6, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     else if (maxm <= 29)
         hipLaunchKernelGGL((k_group_key<8, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
@@ -281,8 +287,9 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
         hipLaunchKernelGGL((k_group_key<25, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // each lane unpacks its pattern into `cap` bytes of LDS: the longest batch's length, 4-byte aligned
+    // (raw records: the search reads the patterns' bytes from HBM, no LDS copy)
     uint32_t cap = 4;
-    for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
+    for (uint32_t j = 0; j < grp.n && !raw; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
     if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair, ix->grouped_xcd, stream)) !=
         hipSuccess)
         return e;
@@ -294,12 +301,17 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
 }
 
 // Bits per packed symbol for a grouped launch of `grp`, or 0 when it cannot
-// be grouped: every batch fixed-length with its patterns within kGroupPackBits.
-static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup &grp) {
+// be grouped (a batch without the fixed-length hint); *raw: some batch's
+// patterns do not pack into kGroupPackBits, so the sorted records carry
+// pattern ids alone (FMX_GROUPED_RAW=1 forces that for every launch).
+static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup &grp, bool *raw) {
     uint32_t bits = 1;
     while ((1u << bits) < ix->bv.sigma + 1) ++bits;
-    for (uint32_t j = 0; j < grp.n; ++j)
-        if (grp.b[j].stride == 0 || grp.b[j].stride * bits > kGroupPackBits) return 0;
+    *raw = ix->grouped_raw;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        if (grp.b[j].stride == 0) return 0;
+        if (grp.b[j].stride * bits > kGroupPackBits) *raw = true;
+    }
     return bits;
 }
 
@@ -313,10 +325,11 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
         grp.b[j].first = total;
         total += grp.b[j].npat;
     }
-    const uint32_t bits = group_pack_bits(ix, grp);
+    bool raw = false;
+    const uint32_t bits = group_pack_bits(ix, grp, &raw);
     const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= ix->grouped_min && !grp.tile_ctr &&
                          search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
-    hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, tiles, total, sb, bits, stream)
+    hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, tiles, total, sb, bits, raw, stream)
                            : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;

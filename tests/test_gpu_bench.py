@@ -79,13 +79,18 @@ def test_gloo_two_ranks_one_gpu_strong():
 
 
 def test_gloo_two_ranks_weak_gather():
-    """c2-style weak scaling on two ranks (gloo, one GPU): after the timed
-    region every batch is gathered in one exactly sized collective and this
-    rank's part comes back intact."""
+    """c2-style weak scaling on two ranks (gloo, one GPU): every launch
+    group's results are all-gathered inside the timed step (one collective
+    per launch, exactly sized slabs), the job assembled on the device holds
+    this rank's part intact, and the padding stays under 1.25x."""
     p = run_bench(["--gpus", "2", "--config", "c2", "--text-len", "20000000", "--patterns", "20000",
                    "--steps", "16", "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
                   env_extra={"FMX_BENCH_BACKEND": "gloo"})
     assert p.returncode == 0, p.stderr[-3000:]
     r = last_json(p.stdout)
     assert r["ranks"] == 2 and r["n_gpus"] == 1 and r["scaling"] == "weak"
-    assert r["gather"]["roundtrip_ok"] and r["gather"]["bytes_gathered"] <= 1.25 * r["gather"]["result_bytes"]
+    g = r["gather"]
+    assert g["inside_timed_step"] and g["collectives_per_launch"] == 1 and g["assembly_ok"]
+    assert g["bytes_gathered_per_pass"] <= 1.25 * g["result_bytes_per_pass"]
+    assert g["assembled_patterns"] == 2 * r["config"]["distinct_batches"] * 20000
+    assert 0 < r["value"] <= g["value_compute_only"] * 1.5

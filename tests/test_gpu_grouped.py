@@ -179,3 +179,44 @@ def test_default_policy_by_alphabet(pkg, O, monkeypatch):
         assert info["group_key_len"] == want_len and info["group_key_base"] == len(chars)
         assert (info["grouped_min"] == 131072) == on
         ix.close()
+
+
+@pytest.mark.parametrize("pb,planes,vb", ALL_LAYOUTS)
+def test_every_layout_grouped_raw(pkg, O, grouped, monkeypatch, pb, planes, vb):
+    """Grouped launches with id-only sorted records (FMX_GROUPED_RAW=1 forces
+    the long-pattern path on patterns that would pack): the key pass reads
+    only the key's bytes, the search reads each pattern's bytes; the smallest
+    and the largest alphabet of the sweep at m = 2 and 7, forward and
+    reversed, blob layout and interleaved records."""
+    monkeypatch.setenv("FMX_GROUPED_RAW", "1")
+    rng = np.random.default_rng(pb * 31 + planes * 7 + vb + 1)
+    for sigma in sorted({2, 1 << planes}):
+        chars = rand_chr_list(rng, sigma)
+        table = table_from_symbols([bytes([c]) for c in chars])
+        text = rand_text(rng, chars, 300, 4000)
+        k, sr = int(rng.integers(1, 5)), int(rng.integers(1, 5))
+        if (sigma + 1) ** k > 1 << 20:
+            k = 2
+        blob = T.gpu_build(pkg, text, sigma, pb, planes, vb, k, sr, table)
+        for m in (2, 7):
+            pats = [rand_pattern(rng, text, m, m) for _ in range(300)]
+            pats = [p for p in pats if len(p) == m]
+            pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=m)) for _ in range(30)]
+            for occ in (0, 1):
+                T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+
+
+@pytest.mark.parametrize("m,pb,planes,vb", [(150, 8, 3, 128), (150, 4, 3, 64), (97, 4, 3, 64), (33, 8, 4, 32)])
+def test_long_patterns_grouped(pkg, O, grouped, m, pb, planes, vb):
+    """C5's shape: patterns too long to pack into a 96-bit record (150 bp)
+    are grouped with id-only records, on a 2 Mbp ACGT text with the ACGTN
+    table; 20,000 cut patterns + absent, wildcard and single-symbol ones,
+    forward and reversed, every count and location against the oracle."""
+    rng = np.random.default_rng(m * 13 + pb)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=2_000_000).astype(np.uint8).tobytes()
+    blob = T.gpu_build(pkg, text, 5, pb, planes, vb, 3, 2, table)
+    pats = [text[s:s + m] for s in rng.integers(0, len(text) - m, size=20_000)]
+    pats += [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=m)) for _ in range(200)]
+    pats += [b"N" * m, b"A" * m, b"\x00" * m]
+    T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1)

@@ -40,6 +40,8 @@ def simt(pkg):
         f.argtypes = args
     L.simt_config.argtypes = [C.c_uint64, C.c_double]
     L.simt_config.restype = None
+    L.simt_stats.argtypes = [C.POINTER(C.c_uint64)] * 3
+    L.simt_stats.restype = None
     saved = n._lib
     n._lib = L
     yield L
@@ -121,10 +123,12 @@ def test_every_layout_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
         if not (sigma == sig[-1] and m in (k, 7)):
             continue
         blob = O.build(text, sigma, O.layout(pb, planes, vb), k, sr, table)
-        for grouped in ("1", "0"):
-            monkeypatch.setenv("FMX_GROUPED", grouped)
+        for grouped in ("1", "raw", "0"):
+            # "raw": grouped with id-only sorted records (the search reads the pattern bytes)
+            monkeypatch.setenv("FMX_GROUPED", "0" if grouped == "0" else "1")
+            monkeypatch.setenv("FMX_GROUPED_RAW", "1" if grouped == "raw" else "0")
             for occ in (0, 1):
-                check_simt(pkg, O, blob, pb, planes, vb, pats[:150] + pats[-43:], occ, reversed_too=grouped == "1")
+                check_simt(pkg, O, blob, pb, planes, vb, pats[:150] + pats[-43:], occ, reversed_too=grouped != "0")
 
 
 def test_group_launch_garbage_workspaces_simt(pkg, O, simt, monkeypatch):
@@ -174,3 +178,31 @@ def test_group_launch_garbage_workspaces_simt(pkg, O, simt, monkeypatch):
             assert int(b["need"][0]) == wl.size
             assert np.array_equal(b["cnt"].view(np.uint32), np.diff(wo).astype(np.uint32))
     ix.close()
+
+
+@pytest.mark.parametrize("m,pb,planes,vb", [(150, 8, 3, 128), (97, 4, 3, 64), (33, 4, 3, 32)])
+def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb):
+    """Patterns too long to pack into a 96-bit record (C5: 150 bp) are grouped
+    with id-only records: the key pass reads only the key's bytes, the search
+    reads each pattern's bytes itself; forward and reversed, against the
+    oracle."""
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    simt.simt_config(m * 7 + pb, 0.5)
+    rng = np.random.default_rng(m)
+    chars = b"ACGT"
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(chars, np.uint8), size=20_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(pb, planes, vb), 3, 2, table)
+    pats = [rand_pattern(rng, text, m, m) for _ in range(300)]
+    pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=m)) for _ in range(20)]
+    pats += [b"N" * m, b"A" * m]
+    g0 = grids(simt)
+    check_simt(pkg, O, blob, pb, planes, vb, pats, 1, reversed_too=False)
+    assert grids(simt) - g0 == 7, "not a grouped launch (load: relayout; locate: key, scan, place, search, tiles, emit)"
+    check_simt(pkg, O, blob, pb, planes, vb, pats, 1)
+
+
+def grids(simt):
+    g, i, s = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    simt.simt_stats(C.byref(g), C.byref(i), C.byref(s))
+    return g.value
