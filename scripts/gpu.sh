@@ -10,6 +10,10 @@
 #   pmc      rocprofv3 PMC passes (FETCH/WRITE size, memory-side requests) on bench.py --streams 1
 #   configs  bench.py --config c1 / c3 / c4 / c5
 #   cli      bench_cli.py: generate, build, locate warm / cold / O_DIRECT (the README workload)
+#   c5ab     C5 grouped at 16 per launch (whole job verified) and in launch order
+#   grouped  pytest tests/test_gpu_grouped.py only
+#   presort  bench.py --presorted (L = 8, 12) and the same command without (upper bound of a longer key)
+#   refineab k_group_refine on / off, alternating twice
 #   gloo2    bench.py --gpus 2 over gloo on the one GPU (the multi-rank path: in-step gathers)
 # Every step has its own time limit; the first failing step ends the run.
 # Output: gpurun_out/TAG/*.
@@ -36,6 +40,22 @@ for step in "$@"; do
             run bench_default 400 python -u bench.py || exit 1
             run bench_driver 400 python -u bench.py --steps 20 --warmup 5 || exit 1 ;;
         single) run bench_single 300 python -u bench.py --single-batch-only || exit 1 ;;
+        c5ab)  # C5 grouped (id-only records) vs launch order, 8 and 16 batches per launch
+            run bench_c5_g16 600 python -u bench.py --config c5 --group 16 --verify-job || exit 1
+            FMX_GROUPED=0 run bench_c5_lo 600 python -u bench.py --config c5 || exit 1 ;;
+        grouped) run pytest_grouped 600 python -u -m pytest tests/test_gpu_grouped.py -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+        presort)  # upper bound of a longer sort key: each launch group pre-sorted by its last L symbols
+            for L in 8 12; do
+                run "bench_presort$L" 400 python -u bench.py --presorted --presort-symbols $L --no-cpu --no-blob-layout \
+                    --no-single-batch || exit 1
+            done
+            run bench_presort_ref 400 python -u bench.py --no-cpu --no-blob-layout --no-single-batch || exit 1 ;;
+        refineab)  # per-key refine sort on / off, alternating, same box
+            for r in 1 2; do
+                run "bench_refine_on$r" 400 python -u bench.py --no-cpu --no-blob-layout --no-single-batch || exit 1
+                FMX_GROUP_REFINE=0 run "bench_refine_off$r" 400 python -u bench.py --no-cpu --no-blob-layout \
+                    --no-single-batch || exit 1
+            done ;;
         gloo2) FMX_BENCH_BACKEND=gloo run bench_gloo2 600 python -u bench.py --gpus 2 --no-cpu || exit 1 ;;
         trace)
             run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run --output-format csv -- \

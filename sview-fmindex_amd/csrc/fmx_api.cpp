@@ -314,6 +314,9 @@ static int status_slot_locked(fmx_index *ix, hipStream_t s, bool launch) {
             if (hipDeviceSynchronize() != hipSuccess) return -1;
             for (auto &sl : ix->slots)
                 if (!sl.inflight) { sl.maybe_busy = false; sl.launched = false; }
+            // (every word is known idle now: completion events are needed again
+            // only once the words run short anew)
+            ix->status_pressure = false;
             idx = pick_recyclable(ix);
         }
         if (idx < 0) return -1;
@@ -483,6 +486,9 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (const char *e = getenv("FMX_GROUPED_PAIR")) ix->grouped_pair = e[0] == '1';
     ix->grouped_raw = false;
     if (const char *e = getenv("FMX_GROUPED_RAW")) ix->grouped_raw = e[0] == '1';
+    ix->group_refine_min = 131072;
+    if (const char *e = getenv("FMX_GROUP_REFINE_MIN")) ix->group_refine_min = strtoull(e, nullptr, 10);
+    if (const char *e = getenv("FMX_GROUP_REFINE")) if (e[0] == '0') ix->group_refine_min = ~0ull;
     if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
         // the largest K with S^K * 2P <= budget, deeper than the blob's k;
         // budget: FMX_DEEP_LUT_MB, else 160 GiB capped at half the free HBM
@@ -787,7 +793,7 @@ fmx_status fmx_load_file(const char *path, fmx_layout layout, int device, uint32
         if (dfd >= 0) close(dfd);
     };
     struct stat sb;
-    if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close(fd); return FMX_E_ARG; }
+    if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) { close_all(); return FMX_E_ARG; }
     const uint64_t blob_len = (uint64_t)sb.st_size;
     LoadTrace tr;
     BlobView bv;
@@ -1017,6 +1023,8 @@ fmx_status fmx_stream_release(fmx_index *ix, void *stream) {
         sl.maybe_busy = false;
         ix->free_slots.push_back(it->second);
         ix->status_of.erase(it);
+        // pressure mode ends once most words are free again
+        if (ix->free_slots.size() >= ix->slots.size() / 2) ix->status_pressure = false;
     }
     return st;
 }

@@ -163,6 +163,9 @@ struct fmx_index {
     uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
     uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
     bool grouped_raw = false;  // FMX_GROUPED_RAW=1: id-only sorted records even for patterns that pack (A/B)
+    // grouped launches of at least this many patterns re-sort each key's run by the next gkey_len
+    // symbols (k_group_refine; FMX_GROUP_REFINE_MIN, FMX_GROUP_REFINE=0: never)
+    uint64_t group_refine_min = 131072;
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -268,6 +271,7 @@ constexpr uint32_t kGroupKeyBits = FMX_GROUP_KEY_BITS;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
 constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key / place workgroup
 constexpr uint32_t kGroupPackBits = 96;
+constexpr uint32_t kGroupRawStage = 216;  // raw records: patterns up to this long are staged in LDS by the search
 constexpr uint32_t kGroupCounterRoom = kGroupBins;
 constexpr uint64_t kWsHeader = 256 + 4ull * kGroupCounterRoom;
 inline uint64_t group_chunks(uint64_t n) { return ((n + 255) / 256 + kGroupChunkTiles - 1) / kGroupChunkTiles; }

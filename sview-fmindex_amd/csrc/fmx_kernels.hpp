@@ -597,6 +597,135 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     }
 }
 
+// 3b. Refine (packed records): the run of each key in the sorted order —
+// the patterns sharing their last gkey_len symbols — re-sorted by their next
+// gkey_len symbols, the nearest one most significant (one workgroup per key;
+// a run longer than kRefineSeg records is sorted in independent segments).
+// Patterns sharing up to 2 gkey_len last symbols (C2: 12) are then searched
+// side by side, so their LF steps below the key read the same records in
+// the same wave instructions or from L2: the bench's --presorted upper
+// bound is +24 / +31 % for 8 / 12 sorted symbols at 25.6 M patterns per
+// launch.  An LDS counting sort; in place: every record of a
+// segment is in registers before any is written back.  After k_group_key
+// <place> the key counters hold each run's end (run k = [cnt[k-1], cnt[k])).
+// Workgroup b takes keys b, b + grid, ... (a smaller launch, fewer workgroups).
+constexpr uint32_t kRefinePer = 8;  // records per thread and segment
+constexpr uint32_t kRefineSeg = 1024 * kRefinePer;
+
+// symbol j of a packed record (bits each)
+__device__ __forceinline__ uint32_t packed_sym(const U4 &e, uint32_t j, uint32_t bits) {
+    const uint64_t lo = (uint64_t)e.x | ((uint64_t)e.y << 32), hi = e.z;
+    const uint32_t at = j * bits;
+    uint64_t x;
+    if (at < 64) {
+        x = lo >> at;
+        if (at + bits > 64) x |= hi << (64 - at);
+    } else {
+        x = hi >> (at - 64);
+    }
+    return (uint32_t)(x & ((1u << bits) - 1u));
+}
+
+template <int UNUSED = 0>
+__global__ __launch_bounds__(1024, 2) void k_group_refine(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
+    constexpr uint32_t T = 1024, per = kGroupBins / T, NW = T / 64;
+    __shared__ uint32_t hist[kGroupBins];
+    __shared__ U4 *s_sorted[kMaxGroup];
+    __shared__ uint64_t s_first[kMaxGroup];
+    __shared__ uint32_t s_vfirst[kMaxGroup], s_stride[kMaxGroup];
+    __shared__ uint8_t s_dig[kMaxSigma + 1];
+    __shared__ uint32_t s_pw[32];
+    __shared__ uint32_t s_wsum[NW];
+    const uint32_t t = threadIdx.x;
+    const uint64_t total = grp.gtotal;
+    if (t < grp.n) {
+        s_sorted[t] = group_sorted(grp.b[t], rec_bytes);
+        s_first[t] = grp.b[t].first;
+        s_vfirst[t] = grp.tile_begin[t] * 256u;
+        s_stride[t] = grp.b[t].stride;
+    }
+    const uint32_t sym_max = a.sigma, L = grp.gkey_len, bits = grp.gbits;
+    if (t <= (uint32_t)kMaxSigma) s_dig[t] = t < sym_max && a.dlut_dig[t] != kNoDigit ? a.dlut_dig[t] : 0;
+    if (t == 0) {
+        uint32_t w = 1;
+        for (uint32_t e = 0; e < 32; ++e) {
+            s_pw[e] = w;
+            w = e + 1 < L ? w * grp.gkey_base : w;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = blockIdx.x; k < kGroupBins; k += gridDim.x) {
+    uint64_t end = grp.gcount[k], beg = k ? grp.gcount[k - 1] : 0;
+    end = end < total ? end : total;
+    beg = beg < end ? beg : end;
+    if (end - beg < 2) continue;  // (workgroup-uniform)
+    for (uint64_t s0 = beg; s0 < end; s0 += kRefineSeg) {
+        const uint64_t sn = end - s0 < kRefineSeg ? end - s0 : kRefineSeg;
+#pragma unroll
+        for (uint32_t u = 0; u < per; ++u) hist[u * T + t] = 0;
+        __syncthreads();
+        U4 rec[kRefinePer];
+        uint32_t key[kRefinePer], rank[kRefinePer];
+#pragma unroll
+        for (uint32_t u = 0; u < kRefinePer; ++u) {
+            const uint64_t p = s0 + u * T + t;
+            key[u] = rank[u] = 0;
+            if (p >= s0 + sn) continue;
+            const uint32_t js = lds_upper(s_first, grp.n, p);
+            rec[u] = s_sorted[js][p - s_first[js]];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kRefinePer; ++u) {
+            const uint64_t p = s0 + u * T + t;
+            if (p >= s0 + sn) continue;
+            const uint32_t m = s_stride[lds_upper(s_vfirst, grp.n, rec[u].w)];
+            uint32_t k2 = 0;
+            for (uint32_t d = 0; d < L; ++d) {
+                const uint32_t back = L + d;  // 0 = the pattern's last symbol
+                const uint32_t c = back < m ? packed_sym(rec[u], m - 1 - back, bits) : sym_max;
+                k2 += (uint32_t)s_dig[c] * s_pw[L - 1 - d];
+            }
+            key[u] = k2;
+            rank[u] = atomicAdd(&hist[k2], 1u);
+        }
+        __syncthreads();
+        // exclusive scan of the histogram: thread t owns entries [per t, per t + per)
+        uint32_t v[per], sum = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < per; ++u) {
+            v[u] = hist[per * t + u];
+            sum += v[u];
+        }
+        const uint32_t lane = t & 63, wv = t >> 6;
+        uint32_t x = sum;
+#pragma unroll
+        for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t y = __shfl_up(x, dd);
+            if (lane >= dd) x += y;
+        }
+        if (lane == 63) s_wsum[wv] = x;
+        __syncthreads();
+        uint32_t run = x - sum;
+        for (uint32_t w = 0; w < wv; ++w) run += s_wsum[w];
+#pragma unroll
+        for (uint32_t u = 0; u < per; ++u) {
+            hist[per * t + u] = run;
+            run += v[u];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kRefinePer; ++u) {
+            const uint64_t p = s0 + u * T + t;
+            if (p >= s0 + sn) continue;
+            const uint64_t np = s0 + hist[key[u]] + rank[u];
+            const uint32_t js = lds_upper(s_first, grp.n, np);
+            s_sorted[js][np - s_first[js]] = rec[u];
+        }
+        __syncthreads();  // (the next segment's histogram)
+    }
+    }
+}
+
 // What k_search_grouped needs of each batch, staged in LDS (the batch of a
 // lane's pattern is per lane here, not per workgroup).
 template <typename P>
@@ -684,10 +813,37 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         pj[q] = jb;
         pi[q] = (uint64_t)(v - s_vfirst[jb]);
         pv[q].m = sb[jb].stride;
-        if (grp.graw) {  // the pattern's own bytes (input order), encoded on each access
-            pv[q].raw = sb[jb].bytes + pi[q] * sb[jb].stride;
-            pv[q].rev = sb[jb].rev != 0;
-            pv[q].sym = nullptr;
+        if (grp.graw) {
+            const uint32_t m = sb[jb].stride;
+            const uint8_t *src = sb[jb].bytes + pi[q] * m;
+            if (cap >= m) {
+                // the pattern's bytes (input order) into its cap bytes of LDS,
+                // encoded, in pattern order: aligned 16-B vectors, four in
+                // flight per round trip (grp.graw with m <= kGroupRawStage)
+                const uint64_t a = reinterpret_cast<uint64_t>(src), a0 = a & ~15ull;
+                const uint32_t lead = (uint32_t)(a - a0), nv = (lead + m + 15) >> 4;
+                const bool rv = sb[jb].rev != 0;
+                const U4 *vp = reinterpret_cast<const U4 *>(a0);
+                for (uint32_t v0 = 0; v0 < nv; v0 += 4) {
+                    U4 x[4];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; ++u)
+                        if (v0 + u < nv) x[u] = vp[v0 + u];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; ++u) {
+                        if (v0 + u >= nv) continue;
+#pragma unroll
+                        for (uint32_t w = 0; w < 16; ++w) {
+                            const uint32_t pos = 16u * (v0 + u) + w - lead;  // (wraps below 0: skipped)
+                            if (pos < m) dst[rv ? m - 1 - pos : pos] = s.enc[(x[u][w >> 2] >> (8 * (w & 3))) & 0xffu];
+                        }
+                    }
+                }
+            } else {  // longer than the LDS room: the bytes from HBM, encoded on each access
+                pv[q].raw = src;
+                pv[q].rev = sb[jb].rev != 0;
+                pv[q].sym = nullptr;
+            }
         } else {
             grouped_unpack<P>(e, sb[jb].stride, grp.gbits, dst);
         }

@@ -115,7 +115,7 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
     return disp(vb, rec, [&]<int VB, int R>() {
         const uint32_t per = pair ? 512u : 256u;
         const uint64_t grid = (total + per - 1) / per;
-        if (grid == 0 || grid > 0x7FFFFFFFull || cap == 0 || cap > kGroupPackBits) return hipErrorInvalidValue;
+        if (grid == 0 || grid > 0x7FFFFFFFull || cap == 0 || cap > kGroupRawStage) return hipErrorInvalidValue;
         if (pair)
             hipLaunchKernelGGL((k_search_grouped<P, N, VB, R, 2>), dim3((uint32_t)grid), dim3(256),
                                512 * cap + qa.kt_lds_bytes, s, qa, grp, total, cap, xcd);

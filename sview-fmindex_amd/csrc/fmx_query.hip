@@ -286,11 +286,20 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     else
         hipLaunchKernelGGL((k_group_key<25, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // each lane unpacks its pattern into `cap` bytes of LDS: the longest batch's length, 4-byte aligned
-    // (raw records: the search reads the patterns' bytes from HBM, no LDS copy)
+    if (!raw && total >= ix->group_refine_min) {
+        // one workgroup per key from 4,096 patterns per key on average (C2's 25.6 M: every key its own)
+        const uint32_t rg = (uint32_t)std::min<uint64_t>(kGroupBins, std::max<uint64_t>(1, total / 4096));
+        hipLaunchKernelGGL(k_group_refine<0>, dim3(rg), dim3(1024), 0, stream, qa, grp, rb);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // each lane unpacks (or, raw, stages) its pattern into `cap` bytes of LDS: the longest batch's length,
+    // 4-byte aligned (raw records longer than kGroupRawStage: the search reads the bytes from HBM, cap 4)
     uint32_t cap = 4;
-    for (uint32_t j = 0; j < grp.n && !raw; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
-    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair, ix->grouped_xcd, stream)) !=
+    for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
+    if (raw && cap > kGroupRawStage) cap = 4;
+    // (two patterns per lane: packed records only — 512 lanes' staging would not fit LDS)
+    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair && !raw, ix->grouped_xcd,
+                                   stream)) !=
         hipSuccess)
         return e;
     if (p4)

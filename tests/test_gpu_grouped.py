@@ -7,7 +7,8 @@ small, so the parity tests below run the key / sorted-order / grouped-search
 / count kernels on fixed-length batches of every layout and alphabet size,
 forward and reversed, with absent, wildcard and out-of-alphabet symbols,
 several batches per launch and many launches on one workspace — each result
-against the oracle (or the host API with grouping off)."""
+against the oracle (or the host API with grouping off).  FMX_GROUP_REFINE_MIN=1
+runs the per-key refine sort (k_group_refine) on all of them too."""
 import numpy as np
 import pytest
 
@@ -20,6 +21,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture
 def grouped(monkeypatch):
     monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")  # k_group_refine on every grouped launch, however small
 
 
 def pack_bits(sigma):

@@ -180,7 +180,7 @@ def test_group_launch_garbage_workspaces_simt(pkg, O, simt, monkeypatch):
     ix.close()
 
 
-@pytest.mark.parametrize("m,pb,planes,vb", [(150, 8, 3, 128), (97, 4, 3, 64), (33, 4, 3, 32)])
+@pytest.mark.parametrize("m,pb,planes,vb", [(150, 8, 3, 128), (97, 4, 3, 64), (33, 4, 3, 32), (250, 4, 3, 64)])
 def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb):
     """Patterns too long to pack into a 96-bit record (C5: 150 bp) are grouped
     with id-only records: the key pass reads only the key's bytes, the search
@@ -206,3 +206,25 @@ def grids(simt):
     g, i, s = C.c_uint64(), C.c_uint64(), C.c_uint64()
     simt.simt_stats(C.byref(g), C.byref(i), C.byref(s))
     return g.value
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_grouped_refine_simt(pkg, O, simt, monkeypatch, seed):
+    """k_group_refine (each key's run re-sorted by the next key-length
+    symbols): a launch of 3,000 fixed-length 16-bp patterns on a 4 kbp text
+    (runs of a few records per key), forward and reversed; and one whose
+    runs exceed a refine segment (8,192 records: 24,000 copies of three
+    patterns, 9 variants of each in their next symbols); against the
+    oracle."""
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")
+    simt.simt_config(4242 + seed, 0.5)
+    rng = np.random.default_rng(99 + seed)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
+    pats = [text[s:s + 16] for s in rng.integers(0, len(text) - 16, size=3_000)]
+    check_simt(pkg, O, blob, 4, 3, 64, pats, 1)
+    base = [text[s:s + 16] for s in rng.integers(0, len(text) - 16, size=3)]
+    var = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=10)) + b[10:] for b in base for _ in range(9)]
+    check_simt(pkg, O, blob, 4, 3, 64, [var[i % len(var)] for i in range(24_000)], 1, reversed_too=False)
