@@ -755,8 +755,11 @@ def main():
     search_us = ks["total_ms"] / ks["launches"] * 1e3 if ks.get("launches") else float("nan")
     k_achieved = alg_per_pattern * ppl / (search_us * 1e-6) / 1e9
     key = f"{args.config}:{n}:{B}:{m}:{info['options']}:g{GR}"
+    # (the engine's policy: packable fixed-length launches from grouped_min patterns; longer patterns only
+    # when FMX_GROUPED=1 / FMX_GROUPED_RAW=1 ask for it)
+    packs = m * table.symbol_count().bit_length() <= 96 and os.environ.get("FMX_GROUPED_RAW") != "1"
     grouped = bool(info.get("group_key_len")) and B * GR >= info["grouped_min"] and bool(fixed) and \
-        m * table.symbol_count().bit_length() <= 96
+        (packs or os.environ.get("FMX_GROUPED") == "1" or os.environ.get("FMX_GROUPED_RAW") == "1")
     tr = traffic_of(args.traffic_json, key)
     roof = {
         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

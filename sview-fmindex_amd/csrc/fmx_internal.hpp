@@ -163,9 +163,11 @@ struct fmx_index {
     uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
     uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
     bool grouped_raw = false;  // FMX_GROUPED_RAW=1: id-only sorted records even for patterns that pack (A/B)
+    uint64_t grouped_raw_min = ~0ull;  // launches needing id-only records: grouped from this many (default never)
     // grouped launches of at least this many patterns re-sort each key's run by the next gkey_len
-    // symbols (k_group_refine; FMX_GROUP_REFINE_MIN, FMX_GROUP_REFINE=0: never)
-    uint64_t group_refine_min = 131072;
+    // symbols (k_group_refine; default never — measured even on C2 —, FMX_GROUP_REFINE_MIN sets it,
+    // FMX_GROUP_REFINE=0: never)
+    uint64_t group_refine_min = ~0ull;
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;

@@ -603,13 +603,14 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
 // a run longer than kRefineSeg records is sorted in independent segments).
 // Patterns sharing up to 2 gkey_len last symbols (C2: 12) are then searched
 // side by side, so their LF steps below the key read the same records in
-// the same wave instructions or from L2: the bench's --presorted upper
-// bound is +24 / +31 % for 8 / 12 sorted symbols at 25.6 M patterns per
-// launch.  An LDS counting sort; in place: every record of a
+// the same wave instructions or from L2.  Opt-in (FMX_GROUP_REFINE_MIN): on
+// C2 at 25.6 M patterns per launch it takes 462 us and saves 352 us of
+// k_search_grouped (the bench's --presorted +31 % comes mostly
+// from result writes in pattern order, which no internal order can give).  An LDS counting sort; in place: every record of a
 // segment is in registers before any is written back.  After k_group_key
 // <place> the key counters hold each run's end (run k = [cnt[k-1], cnt[k])).
 // Workgroup b takes keys b, b + grid, ... (a smaller launch, fewer workgroups).
-constexpr uint32_t kRefinePer = 8;  // records per thread and segment
+constexpr uint32_t kRefinePer = 4;  // records per thread and segment
 constexpr uint32_t kRefineSeg = 1024 * kRefinePer;
 
 // symbol j of a packed record (bits each)
@@ -627,7 +628,7 @@ __device__ __forceinline__ uint32_t packed_sym(const U4 &e, uint32_t j, uint32_t
 }
 
 template <int UNUSED = 0>
-__global__ __launch_bounds__(1024, 2) void k_group_refine(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
+__global__ __launch_bounds__(1024) void k_group_refine(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
     constexpr uint32_t T = 1024, per = kGroupBins / T, NW = T / 64;
     __shared__ uint32_t hist[kGroupBins];
     __shared__ U4 *s_sorted[kMaxGroup];

@@ -336,7 +336,8 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
     }
     bool raw = false;
     const uint32_t bits = group_pack_bits(ix, grp, &raw);
-    const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= ix->grouped_min && !grp.tile_ctr &&
+    const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= (raw ? ix->grouped_raw_min : ix->grouped_min) &&
+                         !grp.tile_ctr &&
                          search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
     hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, tiles, total, sb, bits, raw, stream)
                            : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
