@@ -227,18 +227,21 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
  * [256 B][16 KiB of key counters][tile counts][tile offsets][one search
- * record per pattern][one 16-B sorted-order record per pattern].  A
- * workspace is zeroed by the caller before its first use, then belongs to
- * this index: its launches are ordered on one stream at a time (every launch
- * leaves the key counters zero again).  A locate is k_search + k_emit.  A
+ * record per pattern][to 16 B][one 16-B sorted-order record per pattern].
+ * A workspace needs no initialisation (a grouped launch zeroes its key
+ * counters on its stream first; only the FMX_SEARCH_PERSISTENT=1 A/B variant
+ * wants its first 4 bytes zero) and belongs to this index: its launches are
+ * ordered on one stream at a time.  A locate is k_search + k_emit.  A
  * grouped locate first deals the launch's patterns out in the order of their
  * last symbols, so that patterns whose backward searches share their first
  * LF steps run side by side, and searches them in that order — same
  * results.  Grouped by default: launches (a group call's batches together) of
  * at least 131,072 fixed-length patterns that pack into 96 bits, on the
  * faithful index, when the key spans at least 5 symbols (DNA: 6; environment
- * at load: FMX_GROUPED=0 never, =1 always, FMX_GROUPED_MIN=<patterns>).  No
- * kernel makes one workgroup wait on another. */
+ * at load: FMX_GROUPED=0 never, =1 always — longer patterns too, with
+ * id-only records —, FMX_GROUPED_MIN=<patterns>, FMX_GROUPED_RAW=1 id-only
+ * records, FMX_GROUP_REFINE_MIN=<patterns> re-sorts each key's run by the
+ * next symbols).  No kernel makes one workgroup wait on another. */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)
