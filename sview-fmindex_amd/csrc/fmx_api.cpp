@@ -186,12 +186,38 @@ static hipEvent_t take_event(fmx_index *ix) {
     return e;
 }
 
-static Timer &timer(fmx_index *ix, const char *name) {
-    for (auto &t : ix->timers)
-        if (t.name == name) return t;
+static int timer(fmx_index *ix, const char *name) {
+    for (size_t i = 0; i < ix->timers.size(); ++i)
+        if (ix->timers[i].name == name) return (int)i;
     ix->timers.push_back(Timer{});
     ix->timers.back().name = name;
-    return ix->timers.back();
+    return (int)ix->timers.size() - 1;
+}
+
+// Fold span sp into its timers (its events have completed) and recycle its events.
+static void fold_span(fmx_index *ix, const TimedSpan &sp) {
+    const hipEvent_t from[3] = {sp.a, sp.a, sp.m}, to[3] = {sp.b, sp.m, sp.b};
+    for (int k = 0; k < 3; ++k) {
+        if (sp.timers[k] < 0) continue;
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, from[k], to[k]);
+        Timer &t = ix->timers[sp.timers[k]];
+        t.ms += ms;
+        t.launches += 1;
+        t.units += sp.units;
+    }
+    ix->event_pool.push_back(sp.a);
+    ix->event_pool.push_back(sp.b);
+    if (sp.m) ix->event_pool.push_back(sp.m);
+}
+
+// Fold the oldest spans that have completed while more than kTimedKeep are
+// pending (caller holds timing_mu).
+static void harvest_spans(fmx_index *ix) {
+    while (ix->spans.size() > kTimedKeep && hipEventQuery(ix->spans.front().b) == hipSuccess) {
+        fold_span(ix, ix->spans.front());
+        ix->spans.pop_front();
+    }
 }
 
 // Bracket one launch with events on its stream when timing is on.
@@ -202,12 +228,13 @@ static hipError_t timed(fmx_index *ix, const char *name, hipStream_t s, uint64_t
         g.unlock();
         return launch();
     }
+    harvest_spans(ix);
     hipEvent_t a = take_event(ix), b = take_event(ix);
     if (!a || !b) return hipErrorOutOfMemory;
     hipEventRecord(a, s);
     hipError_t e = launch();
     hipEventRecord(b, s);
-    timer(ix, name).pending.push_back(TimedSpan{a, b, true, true, units});
+    ix->spans.push_back(TimedSpan{a, nullptr, b, {timer(ix, name), -1, -1}, units});
     return e;
 }
 
@@ -221,14 +248,13 @@ static hipError_t timed_split(fmx_index *ix, const char *name, const char *first
         g.unlock();
         return launch(nullptr);
     }
+    harvest_spans(ix);
     hipEvent_t a = take_event(ix), m = take_event(ix), b = take_event(ix);
     if (!a || !m || !b) return hipErrorOutOfMemory;
     hipEventRecord(a, s);
     hipError_t e = launch(m);
     hipEventRecord(b, s);
-    timer(ix, name).pending.push_back(TimedSpan{a, b, true, true, units});
-    timer(ix, first).pending.push_back(TimedSpan{a, m, false, true, units});
-    timer(ix, second).pending.push_back(TimedSpan{m, b, false, false, units});
+    ix->spans.push_back(TimedSpan{a, m, b, {timer(ix, name), timer(ix, first), timer(ix, second)}, units});
     return e;
 }
 
@@ -842,11 +868,11 @@ void fmx_free(fmx_index *ix) {
     if (!ix) return;
     DeviceGuard dg(ix->device);
     if (ix->stream) hipStreamSynchronize(ix->stream);
-    for (auto &t : ix->timers)
-        for (auto &p : t.pending) {
-            if (p.own_a) hipEventDestroy(p.a);
-            if (p.own_b) hipEventDestroy(p.b);
-        }
+    for (const TimedSpan &sp : ix->spans) {
+        hipEventDestroy(sp.a);
+        hipEventDestroy(sp.b);
+        if (sp.m) hipEventDestroy(sp.m);
+    }
     for (auto e : ix->event_pool) hipEventDestroy(e);
     for (auto &sl : ix->slots)
         if (sl.done) hipEventDestroy(sl.done);
@@ -1168,13 +1194,14 @@ fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
     if (enable < 0) return FMX_E_ARG;
     std::lock_guard<std::mutex> g(ix->timing_mu);
     if (enable) {  // a fresh measurement: totals (and spans not read yet) start from zero
+        for (const TimedSpan &sp : ix->spans) {
+            if (hipEventSynchronize(sp.b) != hipSuccess) return FMX_E_DEVICE;
+            ix->event_pool.push_back(sp.a);
+            ix->event_pool.push_back(sp.b);
+            if (sp.m) ix->event_pool.push_back(sp.m);
+        }
+        ix->spans.clear();
         for (auto &t : ix->timers) {
-            for (const TimedSpan &p : t.pending) {
-                if (hipEventSynchronize(p.b) != hipSuccess) return FMX_E_DEVICE;
-                if (p.own_a) ix->event_pool.push_back(p.a);
-                if (p.own_b) ix->event_pool.push_back(p.b);
-            }
-            t.pending.clear();
             t.launches = 0;
             t.ms = 0.0;
             t.units = 0;
@@ -1189,22 +1216,10 @@ fmx_status fmx_timing_enable(fmx_index *ix, int enable) {
 fmx_status fmx_timing_read(fmx_index *ix, fmx_kernel_timing *out, int max_entries, int *n_entries) {
     if (!ix || !n_entries) return FMX_E_ARG;
     std::lock_guard<std::mutex> g(ix->timing_mu);
-    for (auto &t : ix->timers) {
-        for (const TimedSpan &p : t.pending) {
-            if (hipEventSynchronize(p.b) != hipSuccess) return FMX_E_DEVICE;
-            float ms = 0.f;
-            hipEventElapsedTime(&ms, p.a, p.b);
-            t.ms += ms;
-            t.launches += 1;
-            t.units += p.units;
-        }
-    }
-    for (auto &t : ix->timers) {  // (events go back to the pool once every timer has read them)
-        for (const TimedSpan &p : t.pending) {
-            if (p.own_a) ix->event_pool.push_back(p.a);
-            if (p.own_b) ix->event_pool.push_back(p.b);
-        }
-        t.pending.clear();
+    while (!ix->spans.empty()) {
+        if (hipEventSynchronize(ix->spans.front().b) != hipSuccess) return FMX_E_DEVICE;
+        fold_span(ix, ix->spans.front());
+        ix->spans.pop_front();
     }
     int k = 0;
     for (auto &t : ix->timers) {

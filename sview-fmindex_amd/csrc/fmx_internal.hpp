@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -100,21 +101,24 @@ constexpr uint32_t kStatusSymbol = 2u;
 constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
 constexpr uint32_t kStatusGroup = 16u;  // a grouped launch's sorted position out of range (never expected)
 
-// One bracketed launch of a timer: events a -> b; own_a / own_b say whether
-// this entry returns the event to the pool when read (a split launch's
-// "search" and "emit" timers share their events with its "locate" timer).
+// One bracketed launch: events a -> b on its stream, and for a split locate
+// launch m between its two phases; timers[0] gets a -> b, timers[1] a -> m
+// and timers[2] m -> b (-1: none).  Spans are folded into their timers as
+// they complete (the oldest first, whenever more than kTimedKeep are
+// pending, so a long timed region does not hold thousands of events) and
+// all of them by fmx_timing_read.
 struct TimedSpan {
-    hipEvent_t a, b;
-    bool own_a, own_b;
+    hipEvent_t a, m, b;
+    int timers[3];
     uint64_t units;
 };
+constexpr size_t kTimedKeep = 64;
 
 struct Timer {
     std::string name;
     uint64_t launches = 0;
     double ms = 0.0;
     uint64_t units = 0;
-    std::vector<TimedSpan> pending;
 };
 
 // A status word's owner: the stream it is assigned to, its recency (for
@@ -186,6 +190,7 @@ struct fmx_index {
     uint32_t timing_every = 1;   // bracket every k-th launch
     uint64_t timing_seq = 0;
     std::vector<fmx::Timer> timers;
+    std::deque<fmx::TimedSpan> spans;  // bracketed launches not folded into their timers yet
     std::vector<hipEvent_t> event_pool;
     std::mutex timing_mu;  // timers, event_pool, timing_seq
     std::mutex mu;         // the host-buffer calls' scratch and workspace

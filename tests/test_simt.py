@@ -228,3 +228,38 @@ def test_grouped_refine_simt(pkg, O, simt, monkeypatch, seed):
     base = [text[s:s + 16] for s in rng.integers(0, len(text) - 16, size=3)]
     var = [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=10)) + b[10:] for b in base for _ in range(9)]
     check_simt(pkg, O, blob, 4, 3, 64, [var[i % len(var)] for i in range(24_000)], 1, reversed_too=False)
+
+
+def test_timing_long_region_simt(pkg, O, simt):
+    """Launch timing over a region of many launches: spans are folded into
+    their timers as they complete (at most a few dozen pending), and every
+    bracketed launch is counted — 150 host-API locates (timer `locate`) and
+    40 split group launches (`locate`, `locate.search`, `locate.emit`)."""
+    simt.simt_config(7, 0.0)
+    rng = np.random.default_rng(3)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=3_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    pats = [text[s:s + 8] for s in rng.integers(0, len(text) - 8, size=20)]
+    ix.timing_enable(True, every=1)
+    for _ in range(150):
+        ix.locate_batch(pats)
+    t = ix.timing_read()
+    # (the first call may run a second pass: its output guess was too small)
+    assert 150 <= t["locate"]["launches"] <= 151 and t["locate"]["units"] == t["locate"]["launches"] * len(pats)
+    data, offsets = pkg.pack_patterns(pats)
+    n = len(pats)
+    ws = np.zeros(ix.locate_workspace_size(n), np.uint8)
+    loff, locs, need = np.zeros(n + 1, np.int64), np.zeros(4096, np.int32), np.zeros(1, np.int64)
+    job = ix.locate_job(data.ctypes.data, offsets.ctypes.data, n, loff.ctypes.data, locs.ctypes.data, 4096,
+                        need.ctypes.data, ws.ctypes.data, ws.size)
+    q = ix.job_queue([job])
+    ix.timing_enable(True, every=1)
+    for _ in range(40):
+        ix.locate_group_async(q)
+    ix.sync()
+    t = ix.timing_read()
+    assert all(t[k]["launches"] == 40 for k in ("locate", "locate.search", "locate.emit"))
+    ix.timing_enable(False)
+    ix.close()
