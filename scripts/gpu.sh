@@ -14,6 +14,8 @@
 #   grouped  pytest tests/test_gpu_grouped.py only
 #   presort  bench.py --presorted (L = 8, 12) and the same command without (upper bound of a longer key)
 #   refineab k_group_refine on / off, alternating twice
+#   c1ab     C1 at a 2 s and a 0.2 s timed region
+#   knobs    headline A/B: no XCD order, 3 streams, 128 x 4 streams, two patterns per lane
 #   gloo2    bench.py --gpus 2 over gloo on the one GPU (the multi-rank path: in-step gathers)
 # Every step has its own time limit; the first failing step ends the run.
 # Output: gpurun_out/TAG/*.
@@ -56,6 +58,17 @@ for step in "$@"; do
                 FMX_GROUP_REFINE=0 run "bench_refine_off$r" 400 python -u bench.py --no-cpu --no-blob-layout \
                     --no-single-batch || exit 1
             done ;;
+        c1ab)  # C1 (launch-bound) at a 2 s and a 0.2 s timed region
+            run bench_c1_2s 300 python -u bench.py --config c1 --no-cpu || exit 1
+            run bench_c1_02s 300 python -u bench.py --config c1 --no-cpu --min-seconds 0.2 || exit 1 ;;
+        knobs)  # launch-shape and grouping knobs on the headline (no CPU / blob / single legs), same box
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            run knob_ref 300 $B || exit 1
+            FMX_GROUPED_XCD=0 run knob_noxcd 300 $B || exit 1
+            run knob_s3 300 $B --streams 3 || exit 1
+            run knob_g128_s4 300 $B --group 128 --streams 4 || exit 1
+            FMX_GROUPED_PAIR=1 run knob_pair 300 $B || exit 1
+            run knob_ref2 300 $B || exit 1 ;;
         gloo2) FMX_BENCH_BACKEND=gloo run bench_gloo2 600 python -u bench.py --gpus 2 --no-cpu || exit 1 ;;
         trace)
             run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run --output-format csv -- \
