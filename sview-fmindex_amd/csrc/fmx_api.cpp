@@ -523,6 +523,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     ix->group_refine_min = ~0ull;
     if (const char *e = getenv("FMX_GROUP_REFINE_MIN")) ix->group_refine_min = strtoull(e, nullptr, 10);
     if (const char *e = getenv("FMX_GROUP_REFINE")) if (e[0] == '0') ix->group_refine_min = ~0ull;
+    if (const char *e = getenv("FMX_GROUP_CHECK")) ix->group_check = e[0] == '1';
     if ((options & FMX_OPT_DEEP_LUT) && S >= 2 && v.n > 0) {
         // the largest K with S^K * 2P <= budget, deeper than the blob's k;
         // budget: FMX_DEEP_LUT_MB, else 160 GiB capped at half the free HBM
@@ -608,7 +609,13 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
     if (st & kStatusStride) return FMX_E_ARG;
-    if (st & kStatusGroup) return FMX_E_DEVICE;
+    if (st & (kStatusGroup | kStatusCheck)) {
+        static const bool debug = getenv("FMX_DEBUG") != nullptr;
+        if (debug)
+            fprintf(stderr, "fmx: grouped launch: %s\n",
+                    (st & kStatusCheck) ? "sorted order failed FMX_GROUP_CHECK" : "sorted position out of range");
+        return FMX_E_DEVICE;
+    }
     return FMX_OK;
 }
 

@@ -100,6 +100,7 @@ constexpr uint32_t kStatusEmpty = 1u;
 constexpr uint32_t kStatusSymbol = 2u;
 constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
 constexpr uint32_t kStatusGroup = 16u;  // a grouped launch's sorted position out of range (never expected)
+constexpr uint32_t kStatusCheck = 32u;  // FMX_GROUP_CHECK=1: a grouped launch's sorted order failed its check
 
 // One bracketed launch: events a -> b on its stream, and for a split locate
 // launch m between its two phases; timers[0] gets a -> b, timers[1] a -> m
@@ -164,7 +165,7 @@ struct fmx_index {
     // gkey_len symbols, digits over the gkey_base symbols that occur in the text
     uint64_t grouped_min = 0;
     uint32_t gkey_len = 0, gkey_base = 0;
-    uint32_t grouped_xcd = 0;  // FMX_GROUPED_XCD=1: each XCD searches one eighth of the key order
+    uint32_t grouped_xcd = 0;  // each XCD searches one eighth of the key order (default; FMX_GROUPED_XCD=0 off)
     uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
     bool grouped_raw = false;  // FMX_GROUPED_RAW=1: id-only sorted records even for patterns that pack (A/B)
     uint64_t grouped_raw_min = ~0ull;  // launches needing id-only records: grouped from this many (default never)
@@ -172,6 +173,9 @@ struct fmx_index {
     // symbols (k_group_refine; default never — measured even on C2 —, FMX_GROUP_REFINE_MIN sets it,
     // FMX_GROUP_REFINE=0: never)
     uint64_t group_refine_min = ~0ull;
+    // FMX_GROUP_CHECK=1 (debug): every grouped launch checks its sorted order before the search —
+    // each pattern placed exactly once, under its own key, with its own symbols (k_group_check_*)
+    bool group_check = false;
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;

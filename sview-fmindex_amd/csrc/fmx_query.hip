@@ -106,6 +106,95 @@ __global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp) {
     if (threadIdx.x == 0) B.tiles[g] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
+// ------------------------------------------- grouped launches: debug check
+// FMX_GROUP_CHECK=1 (fmx_index::group_check): after the place (and refine)
+// pass and before the search, the launch's sorted order is checked against
+// the patterns themselves — every sorted position holds a pattern id of the
+// launch, each id exactly once (a per-pattern tally in the batch's search
+// records, which the search overwrites afterwards), under the key of the run
+// it sits in (gcount, which after the place pass holds each run's end), and
+// (packed records) with the pattern's own symbols.  A failure latches
+// kStatusCheck (FMX_E_DEVICE; FMX_DEBUG names it).  Three launches; no
+// workgroup waits on another.
+
+__device__ __forceinline__ uint32_t *group_tally(const LocateBatch &B) {
+    return reinterpret_cast<uint32_t *>(B.tiles + 2 * ((B.npat + 255) / 256));
+}
+
+// 1. and 3.: every pattern's tally zeroed / checked to be 1 (one workgroup per tile)
+template <bool ZERO>
+__global__ __launch_bounds__(256) void k_group_check_tally(const QueryArgs a, const LocateGroup grp) {
+    const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t i = (uint64_t)(vt - grp.tile_begin[jb]) * 256u + threadIdx.x;
+    if (i >= B.npat) return;
+    uint32_t *tally = group_tally(B);
+    if (ZERO) tally[i] = 0;
+    else if (tally[i] != 1u) atomicOr(a.status, kStatusCheck);
+}
+
+// 2. each sorted position (one per thread)
+__global__ __launch_bounds__(256) void k_group_check_order(const QueryArgs a, const LocateGroup grp,
+                                                           uint32_t rec_bytes) {
+    __shared__ uint64_t s_first[kMaxGroup];
+    __shared__ uint32_t s_vfirst[kMaxGroup];
+    __shared__ uint8_t s_enc[256];
+    __shared__ uint8_t s_dig[kMaxSigma];
+    __shared__ uint32_t s_pw[32];
+    const uint32_t t = threadIdx.x, L = grp.gkey_len;
+    for (uint32_t j = t; j < grp.n; j += 256) {
+        s_first[j] = grp.b[j].first;
+        s_vfirst[j] = grp.tile_begin[j] * 256u;
+    }
+    s_enc[t] = a.enc[t];
+    if (t < (uint32_t)kMaxSigma) s_dig[t] = a.dlut_dig[t] == kNoDigit ? 0 : a.dlut_dig[t];
+    if (t == 0) {
+        uint32_t w = 1;
+        for (uint32_t e = 0; e < 32; ++e) {
+            s_pw[e] = w;
+            w = e + 1 < L ? w * grp.gkey_base : w;
+        }
+    }
+    __syncthreads();
+    const uint64_t sp = (uint64_t)blockIdx.x * 256u + t, total = grp.gtotal;
+    if (sp >= total) return;
+    bool bad = grp.gcount[kGroupBins - 1] != total;  // (the last run ends at the launch's end)
+    const uint32_t js = lds_upper(s_first, grp.n, sp);
+    const U4 e = group_sorted(grp.b[js], rec_bytes)[sp - s_first[js]];
+    const uint32_t jb = lds_upper(s_vfirst, grp.n, e.w);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t i = (uint64_t)(e.w - s_vfirst[jb]);
+    if (e.w < s_vfirst[jb] || i >= B.npat) {
+        atomicOr(a.status, kStatusCheck);
+        return;
+    }
+    atomicAdd(group_tally(B) + i, 1u);
+    // the run holding sp: the first key whose end is past it
+    uint32_t lo = 0, hi = kGroupBins - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((uint64_t)grp.gcount[mid] > sp) hi = mid;
+        else lo = mid + 1;
+    }
+    const uint32_t m = B.stride;
+    const bool rev = B.rev != 0;
+    const uint8_t *pat = B.bytes + i * m;
+    uint32_t key = 0;
+    for (uint32_t back = 0; back < L && back < m; ++back) {
+        const uint32_t j = m - 1 - back, c = s_enc[pat[rev ? m - 1 - j : j]];
+        key += (c < (uint32_t)kMaxSigma ? s_dig[c] : 0u) * s_pw[L - 1 - back];
+    }
+    bad |= key != lo;
+    if (!grp.graw) {
+        for (uint32_t j = 0; j < m; ++j) {
+            uint32_t c = s_enc[pat[rev ? m - 1 - j : j]];
+            c = c < a.sigma ? c : a.sigma;
+            bad |= packed_sym(e, j, grp.gbits) != c;
+        }
+    }
+    if (bad) atomicOr(a.status, kStatusCheck);
+}
+
 // ------------------------------------------------------------ deep k-mer table
 
 // The table's digits are the S symbols that occur in the text (dlut_sym).
@@ -290,6 +379,13 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
         // one workgroup per key from 4,096 patterns per key on average (C2's 25.6 M: every key its own)
         const uint32_t rg = (uint32_t)std::min<uint64_t>(kGroupBins, std::max<uint64_t>(1, total / 4096));
         hipLaunchKernelGGL(k_group_refine<0>, dim3(rg), dim3(1024), 0, stream, qa, grp, rb);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (ix->group_check) {
+        const uint32_t ord = (uint32_t)((total + 255) / 256);
+        hipLaunchKernelGGL(k_group_check_tally<true>, dim3(tiles), dim3(256), 0, stream, qa, grp);
+        hipLaunchKernelGGL(k_group_check_order, dim3(ord), dim3(256), 0, stream, qa, grp, rb);
+        hipLaunchKernelGGL(k_group_check_tally<false>, dim3(tiles), dim3(256), 0, stream, qa, grp);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // each lane unpacks (or, raw, stages) its pattern into `cap` bytes of LDS: the longest batch's length,

@@ -388,6 +388,16 @@ void simt_config(uint64_t seed, double yield_p) {
     g_rng.seed(seed);
     g_yield = yield_p;
 }
+// TEST hook (fault injection): the next zeroing memset of exactly `size`
+// bytes leaves these words at its start instead of zeros (e.g. a grouped
+// launch's key counters left dirty by a launch cut short).
+static std::vector<uint32_t> g_memset_fault;
+static uint64_t g_memset_fault_size = 0;
+void simt_memset_fault(uint64_t size, const uint32_t *words, uint64_t n_words) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    g_memset_fault.assign(words, words + n_words);
+    g_memset_fault_size = size;
+}
 void simt_stats(uint64_t *grids, uint64_t *items, uint64_t *switches) {
     *grids = g_grids;
     *items = g_items;
@@ -481,14 +491,21 @@ hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hip
     return hipSuccess;
 }
 hipError_t hipMemcpyPeer(void *d, int, const void *s, int, size_t n) { return hipMemcpy(d, s, n, hipMemcpyDefault); }
+static void memset_or_fault(void *d, int v, size_t n) {
+    if (n) std::memset(d, v, n);
+    if (v == 0 && g_memset_fault_size && n == g_memset_fault_size) {
+        std::memcpy(d, g_memset_fault.data(), std::min<size_t>(n, 4 * g_memset_fault.size()));
+        g_memset_fault_size = 0;
+    }
+}
 hipError_t hipMemset(void *d, int v, size_t n) {
     land_pending();
-    if (n) std::memset(d, v, n);
+    memset_or_fault(d, v, n);
     return hipSuccess;
 }
 hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t st) {
     if (null_stream(st)) return hipMemset(d, v, n);
-    if (n) std::memset(d, v, n);
+    memset_or_fault(d, v, n);
     return hipSuccess;
 }
 hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) {

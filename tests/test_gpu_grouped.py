@@ -8,7 +8,10 @@ small, so the parity tests below run the key / sorted-order / grouped-search
 forward and reversed, with absent, wildcard and out-of-alphabet symbols,
 several batches per launch and many launches on one workspace — each result
 against the oracle (or the host API with grouping off).  FMX_GROUP_REFINE_MIN=1
-runs the per-key refine sort (k_group_refine) on all of them too."""
+runs the per-key refine sort (k_group_refine) on all of them too, and
+FMX_GROUP_CHECK=1 checks every launch's sorted order on the device before its
+search (each pattern placed once, under its own key, with its own symbols;
+a violation is FMX_E_DEVICE)."""
 import numpy as np
 import pytest
 
@@ -22,6 +25,7 @@ pytestmark = pytest.mark.gpu
 def grouped(monkeypatch):
     monkeypatch.setenv("FMX_GROUPED", "1")
     monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")  # k_group_refine on every grouped launch, however small
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")  # the device-side check of the sorted order (k_group_check_*)
 
 
 def pack_bits(sigma):

@@ -42,6 +42,8 @@ def simt(pkg):
     L.simt_config.restype = None
     L.simt_stats.argtypes = [C.POINTER(C.c_uint64)] * 3
     L.simt_stats.restype = None
+    L.simt_memset_fault.argtypes = [C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64]
+    L.simt_memset_fault.restype = None
     saved = n._lib
     n._lib = L
     yield L
@@ -102,6 +104,7 @@ def test_grouped_verdict_r3_case(pkg, O, simt, monkeypatch, seed):
     late-landing upload made k_relayout build the records from stale memory
     and this test crashed in the emulator (the GPU read garbage silently)."""
     monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
     simt.simt_config(1000 + seed, 0.5)
     pb, planes, vb = 4, 5, 32
     for sigma, m, text, table, k, sr, pats in grouped_case_inputs(pb, planes, vb, sigma_pick=2, m_pick=2):
@@ -117,6 +120,7 @@ def test_every_layout_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
     smallest alphabet, whose patterns have ~800 occurrences each, runs in the
     round-3 case above)."""
     simt.simt_config(pb * 131 + planes * 17 + vb, 0.5)
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
     cases = list(grouped_case_inputs(pb, planes, vb))
     sig = sorted({c[0] for c in cases})
     for sigma, m, text, table, k, sr, pats in cases:
@@ -138,6 +142,7 @@ def test_group_launch_garbage_workspaces_simt(pkg, O, simt, monkeypatch):
     grouped launch on a garbage workspace) and reused twice: every count,
     offset and location against the oracle each time."""
     monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
     simt.simt_config(77, 0.5)
     rng = np.random.default_rng(34)
     table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
@@ -202,6 +207,59 @@ def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb
     check_simt(pkg, O, blob, pb, planes, vb, pats, 1)
 
 
+GROUP_BINS = 4096  # fmx_internal.hpp kGroupBins: the key counters' 16 KiB
+
+
+def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
+    """Fault injection: the grouped launch's key
+    counters are left dirty, as a launch cut short between its count pass
+    and its end would leave them without the zeroing memset.
+      * -1 in key 0 (ending AAAAAA: three patterns have it) and +1 in the
+        last key: the runs of the keys between shift down by one, two
+        patterns share a sorted position and the last one is never written —
+        every position stays inside the launch, so the place pass's guard
+        passes it (no error without the check) and only FMX_GROUP_CHECK=1
+        sees it: FMX_E_DEVICE;
+      * +5 in key 0: positions run past the launch's end; the place pass's
+        guard refuses them: FMX_E_DEVICE without the check.
+    The index answers correctly again on the next (clean) launch."""
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    simt.simt_config(31337, 0.5)
+    rng = np.random.default_rng(8)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=6_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    pats = [text[s:s + 12] for s in rng.integers(0, len(text) - 12, size=700)] + [b"CCCCCCAAAAAA"] * 3
+    data, offsets = pkg.pack_patterns(pats)
+    want = orc.locate_batch(data, offsets)
+
+    def inject(words):
+        w = (C.c_uint32 * GROUP_BINS)(*words)
+        simt.simt_memset_fault(4 * GROUP_BINS, w, GROUP_BINS)
+
+    shifted = [0] * GROUP_BINS
+    shifted[0], shifted[-1] = 0xFFFFFFFF, 1
+    over = [0] * GROUP_BINS
+    over[0] = 5
+    for check, words, caught in (("1", shifted, True), ("0", shifted, False), ("0", over, True),
+                                 ("1", over, True)):
+        monkeypatch.setenv("FMX_GROUP_CHECK", check)
+        ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+        got = ix.locate_batch((data, offsets))  # clean: the fault is not armed yet
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+        inject(words)
+        if caught:
+            with pytest.raises(pkg.FmxError) as ei:
+                ix.locate_batch((data, offsets))
+            assert ei.value.code == pkg._native.FMX_E_DEVICE
+        else:
+            ix.locate_batch((data, offsets))  # (answers from a broken order: what the check exists for)
+        got = ix.locate_batch((data, offsets))
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), "not clean after the fault"
+        ix.close()
+
+
 def grids(simt):
     g, i, s = C.c_uint64(), C.c_uint64(), C.c_uint64()
     simt.simt_stats(C.byref(g), C.byref(i), C.byref(s))
@@ -218,6 +276,7 @@ def test_grouped_refine_simt(pkg, O, simt, monkeypatch, seed):
     oracle."""
     monkeypatch.setenv("FMX_GROUPED", "1")
     monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
     simt.simt_config(4242 + seed, 0.5)
     rng = np.random.default_rng(99 + seed)
     table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
