@@ -16,6 +16,9 @@
 #   refineab k_group_refine on / off, alternating twice
 #   c1ab     C1 at a 2 s and a 0.2 s timed region
 #   knobs    headline A/B: no XCD order, 3 streams, 128 x 4 streams, two patterns per lane
+#   wsortab  the grouped search's in-workgroup sort by the next symbols on / off (FMX_GROUPED_WSORT=0), twice
+#   emitab   k_emit / k_group_tiles with 4 tiles per workgroup (this build) vs 1 (build_ab/libfmx_e1.so
+#            via FMX_LIB, built with -DFMX_EMIT_TILES=1), alternating twice
 #   gloo2    bench.py --gpus 2 over gloo on the one GPU (the multi-rank path: in-step gathers)
 # Every step has its own time limit; the first failing step ends the run.
 # Output: gpurun_out/TAG/*.
@@ -69,6 +72,22 @@ for step in "$@"; do
             run knob_g128_s4 300 $B --group 128 --streams 4 || exit 1
             FMX_GROUPED_PAIR=1 run knob_pair 300 $B || exit 1
             run knob_ref2 300 $B || exit 1 ;;
+        wsortab)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "wsort_on_$r" 300 $B || exit 1
+                FMX_GROUPED_WSORT=0 run "wsort_off_$r" 300 $B || exit 1
+            done
+            run wsort_on_c4 400 python -u bench.py --config c4 --no-cpu || exit 1
+            FMX_GROUPED_WSORT=0 run wsort_off_c4 400 python -u bench.py --config c4 --no-cpu || exit 1 ;;
+        emitab)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "emit_e4_$r" 300 $B || exit 1
+                FMX_LIB=$PWD/build_ab/libfmx_e1.so run "emit_e1_$r" 300 $B || exit 1
+            done
+            FMX_LIB=$PWD/build_ab/libfmx_e1.so run emit_e1_c1 300 python -u bench.py --config c1 --no-cpu || exit 1
+            run emit_e4_c1 300 python -u bench.py --config c1 --no-cpu || exit 1 ;;
         gloo2) FMX_BENCH_BACKEND=gloo run bench_gloo2 600 python -u bench.py --gpus 2 --no-cpu || exit 1 ;;
         trace)
             run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run --output-format csv -- \

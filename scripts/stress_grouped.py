@@ -4,7 +4,7 @@ for a time budget, and prints every per-pattern mismatch against the oracle
 (layout, sigma, m, load options, direction, which patterns, GPU vs oracle
 count) instead of stopping at the first assert.
 
-    python scripts/stress_grouped.py --seconds 240 [--layouts 4-5-32,4-4-64] [--env FMX_GROUP_CHECK=1]
+    python scripts/stress_grouped.py --seconds 240 [--layouts 4-5-32,4-4-64] [--env FMX_GROUP_CHECK=1] [--rebuild]
 """
 import argparse
 import os
@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--layouts", default="")
     ap.add_argument("--env", action="append", default=[])
     ap.add_argument("--grouped", default="1")
+    ap.add_argument("--rebuild", action="store_true",
+                    help="build every blob on the GPU again each round (as the suite does), not once")
     a = ap.parse_args()
     os.environ["FMX_GROUPED"] = a.grouped
     for kv in a.env:
@@ -45,6 +47,8 @@ def main():
             if time.time() - t0 >= a.seconds:
                 break
             key = (pb, planes, vb)
+            if a.rebuild:
+                cache.pop(key, None)
             if key not in cache:
                 rng = np.random.default_rng(pb * 31 + planes * 7 + vb)
                 cases = []
@@ -92,7 +96,16 @@ def main():
                             print(msg, f"patterns={len(pats)} bad={len(bad)} total gpu={int(goff[-1])} "
                                   f"oracle={int(ooff[-1])}", flush=True)
                             for b in bad[:12]:
-                                print(f"   pat {b} {pats[b]!r} gpu {gc[b]} oracle {oc[b]}", flush=True)
+                                same = sorted({pats[j] for j in np.flatnonzero(oc == gc[b])})[:4]
+                                print(f"   pat {b} {pats[b]!r} gpu {gc[b]} oracle {oc[b]} "
+                                      f"(oracle count of {same!r})", flush=True)
+                                gl = glocs[goff[b]:goff[b + 1]] if not rev else None
+                                if gl is not None and gl.size:
+                                    hits = [(j, pats[j]) for j in range(len(pats)) if pats[j] != pats[b] and
+                                            oc[j] == gc[b] and np.array_equal(np.sort(olocs[ooff[j]:ooff[j + 1]]),
+                                                                              np.sort(gl))]
+                                    print(f"      its locations are pattern {hits[:1]!r}'s" if hits else
+                                          "      its locations match no other pattern's", flush=True)
                             if len(bad) == 0:
                                 d = np.flatnonzero(glocs != olocs)
                                 print(f"   locations differ at {d[:8].tolist()} of {olocs.size}", flush=True)

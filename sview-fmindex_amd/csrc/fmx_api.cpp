@@ -510,6 +510,8 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (const char *e = getenv("FMX_GROUPED_XCD")) ix->grouped_xcd = e[0] == '1';
     ix->grouped_pair = 0;
     if (const char *e = getenv("FMX_GROUPED_PAIR")) ix->grouped_pair = e[0] == '1';
+    ix->grouped_wsort = true;
+    if (const char *e = getenv("FMX_GROUPED_WSORT")) ix->grouped_wsort = e[0] != '0';
     ix->grouped_raw = false;
     if (const char *e = getenv("FMX_GROUPED_RAW")) ix->grouped_raw = e[0] == '1';
     // patterns too long to pack (id-only records) are grouped only on request:

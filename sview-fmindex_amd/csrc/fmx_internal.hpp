@@ -167,6 +167,9 @@ struct fmx_index {
     uint32_t gkey_len = 0, gkey_base = 0;
     uint32_t grouped_xcd = 0;  // each XCD searches one eighth of the key order (default; FMX_GROUPED_XCD=0 off)
     uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
+    // the grouped search sorts each workgroup's 256 patterns by their next symbols after the key
+    // (k_search_grouped; default on, FMX_GROUPED_WSORT=0 off)
+    bool grouped_wsort = true;
     bool grouped_raw = false;  // FMX_GROUPED_RAW=1: id-only sorted records even for patterns that pack (A/B)
     uint64_t grouped_raw_min = ~0ull;  // launches needing id-only records: grouped from this many (default never)
     // grouped launches of at least this many patterns re-sort each key's run by the next gkey_len
@@ -235,6 +238,7 @@ struct LocateBatch {
 struct LocateGroup {
     LocateBatch b[kMaxGroup];
     uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
+    uint32_t emit_begin[kMaxGroup];  // first k_emit / k_group_tiles workgroup of batch j (kEmitTiles tiles each)
     uint32_t n;
     // Grouped launch (kWsHeader below): the group's key counters (batch 0's
     // workspace, zeroed on the launch's stream before its first kernel), the
@@ -257,6 +261,14 @@ hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;
+// k_emit and k_group_tiles take this many tiles of one batch per workgroup:
+// each of their waves has that many record loads in flight instead of one
+// (a workgroup's life is mostly one HBM round trip; 100,000 one-tile
+// workgroups per C2 launch ran ~49 rounds of them).  Build option for A/B.
+#ifndef FMX_EMIT_TILES
+#define FMX_EMIT_TILES 4
+#endif
+constexpr uint32_t kEmitTiles = FMX_EMIT_TILES;
 
 // Grouped launches.  A launch's patterns are searched in the order of their
 // last gkey_len symbols (a counting sort on one key per pattern) instead of
@@ -282,6 +294,8 @@ constexpr uint32_t kGroupKeyBits = FMX_GROUP_KEY_BITS;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
 constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key / place workgroup
 constexpr uint32_t kGroupPackBits = 96;
+constexpr uint32_t kGroupedXcd = 1;  // k_search_grouped opts: deal the key order out XCD by XCD
+constexpr uint32_t kWsortBytes = 1024 + 256 * 16;  // its in-workgroup sort's LDS (256 counters, 256 records)
 constexpr uint32_t kGroupRawStage = 216;  // raw records: patterns up to this long are staged in LDS by the search
 constexpr uint32_t kGroupCounterRoom = kGroupBins;
 constexpr uint64_t kWsHeader = 256 + 4ull * kGroupCounterRoom;
@@ -298,9 +312,10 @@ struct LayoutOps {
                          uint32_t tiles, uint32_t sb, hipStream_t s);
     hipError_t (*emit)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp, uint32_t tiles,
                        uint32_t fold, hipStream_t s);
-    // grouped launch (faithful variant): k_search_grouped over `total` patterns in key order
+    // grouped launch (faithful variant): k_search_grouped over `total` patterns in key order;
+    // opts = kGroupedXcd | wsort << 8 (k_search_grouped)
     hipError_t (*search_grouped)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
-                                 uint64_t total, uint32_t cap, uint32_t pair, uint32_t xcd, hipStream_t s);
+                                 uint64_t total, uint32_t cap, uint32_t pair, uint32_t opts, hipStream_t s);
     hipError_t (*dlut_level)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const void *parent, uint64_t np,
                              void *child, hipStream_t s);
     hipError_t (*full_sa)(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t n, void *sa_out,

@@ -760,16 +760,38 @@ __device__ __forceinline__ void grouped_unpack(const U4 &e, uint32_t m, uint32_t
     }
 }
 
+// The LDS before the k-mer table: each lane's cap bytes of symbols, or the
+// in-workgroup sort's room when that is larger (it is done with before the
+// symbols are unpacked).
+__host__ __device__ constexpr uint32_t grouped_pat_bytes(uint32_t k, uint32_t cap, uint32_t wsort) {
+    return 256u * k * cap > kWsortBytes || !wsort ? 256u * k * cap : kWsortBytes;
+}
+
+// opts bit 0 (kGroupedXcd): the XCD deal below; opts >> 8 = wsort: a full
+// workgroup of packed records (K = 1) first sorts its 256 patterns by their
+// next wsort symbols after the key (digits over the key's base, the nearest
+// symbol most significant; base^wsort <= 256) — an LDS counting sort — so
+// that a wave's lanes share up to gkey_len + 1 or 2 last symbols and the LF
+// steps just below the key read the same lines in the same wave instruction
+// (one request each) instead of up to 64 different ones.  Which lane answers
+// which pattern changes nothing in the results (each is written at its own
+// index).
 template <typename P, int N, int VB, int REC, int K>
 __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const QueryArgs a, const LocateGroup grp,
-                                                           uint64_t total, uint32_t cap, uint32_t xcd) {
+                                                           uint64_t total, uint32_t cap, uint32_t opts) {
     static_assert(K == 1 || K == 2, "one or two patterns per lane");
     __shared__ Tables<P> s;
     __shared__ GroupBatch<P> sb[kMaxGroup];
     __shared__ uint64_t s_first[kMaxGroup];   // the launch's patterns before batch j
     __shared__ uint32_t s_vfirst[kMaxGroup];  // batch j's first pattern id (tile_begin * 256)
+    __shared__ uint8_t s_dig[kMaxSigma + 1];  // (wsort) symbol -> digit; sigma (past the pattern's start) -> 0
+    __shared__ uint64_t s_wscan[4];
+    const uint32_t wsort = K == 1 && !grp.graw ? opts >> 8 : 0u, xcd = opts & kGroupedXcd;
     FMX_DYN_LDS(s_pat);  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
-    stage_tables(a, s, s_pat + 256 * K * cap);
+    stage_tables(a, s, s_pat + grouped_pat_bytes(K, cap, wsort));
+    if (threadIdx.x <= (uint32_t)kMaxSigma)
+        s_dig[threadIdx.x] =
+            threadIdx.x < a.sigma && a.dlut_dig[threadIdx.x] != kNoDigit ? a.dlut_dig[threadIdx.x] : 0;
     for (uint32_t j = threadIdx.x; j < grp.n; j += 256) {
         const LocateBatch &B = grp.b[j];
         const uint64_t G = (B.npat + 255) / 256;
@@ -808,7 +830,30 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         pv[q].sym = dst;
         if (!live[q]) continue;
         const uint32_t js = lds_upper(s_first, grp.n, sp);
-        const U4 e = sb[js].sorted[sp - s_first[js]];
+        U4 e = sb[js].sorted[sp - s_first[js]];
+        if (K == 1 && wsort && (uint64_t)chunk * 256u + 256u <= total) {  // (workgroup-uniform: all lanes live)
+            uint32_t *hist = reinterpret_cast<uint32_t *>(s_pat);
+            U4 *stage = reinterpret_cast<U4 *>(s_pat + 1024);
+            const uint32_t t = threadIdx.x, L = grp.gkey_len, base = grp.gkey_base;
+            const uint32_t m = sb[lds_upper(s_vfirst, grp.n, e.w)].stride;
+            uint32_t k2 = 0;
+            for (uint32_t d = 0; d < wsort; ++d) {
+                const uint32_t back = L + d;  // 0 = the pattern's last symbol
+                k2 = k2 * base + s_dig[back < m ? packed_sym(e, m - 1 - back, grp.gbits) : a.sigma];
+            }
+            hist[t] = 0;
+            __syncthreads();
+            const uint32_t rank = atomicAdd(&hist[k2], 1u);
+            __syncthreads();
+            uint64_t agg;
+            const uint32_t before = (uint32_t)block_excl_scan(hist[t], &agg, s_wscan);
+            hist[t] = before;  // (each thread its own counter; read after the next barrier)
+            __syncthreads();
+            stage[hist[k2] + rank] = e;
+            __syncthreads();
+            e = stage[t];
+            __syncthreads();  // (the stage is s_pat: every lane has its record before any unpacks)
+        }
         const uint32_t v = e.w;
         const uint32_t jb = lds_upper(s_vfirst, grp.n, v);
         pj[q] = jb;
@@ -893,61 +938,101 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
                 NarrowRec<P>{mode[q] == kHitOne ? rloc[q] : lo_r[q], (P)(hi_r[q] - lo_r[q])};
 }
 
+// This workgroup's batch of a k_emit / k_group_tiles launch (workgroup-uniform).
+__device__ __forceinline__ uint32_t emit_batch(const LocateGroup &grp, uint32_t w) {
+    uint32_t lo = 0, hi = grp.n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (grp.emit_begin[mid] <= w) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // 3. Output offsets (tile offset + in-tile scan) and every location, rows
-// dealt across each wave's lanes (emit_locations).
+// dealt across each wave's lanes (emit_locations).  Workgroup w takes tiles
+// [E k, E k + E) of its batch (k = w - emit_begin, E = kEmitTiles): lane t
+// loads its pattern of each of them first, so a wave has E record loads in
+// flight, then answers them tile by tile.
 // fold bit 0: batches of at most kFoldTiles tiles need no k_scan: each
-// workgroup sums the counts of the tiles before its own (all final: k_search
-// is done), and the last tile writes the batch total.  Bit 1: the records are
-// NarrowRec (a grouped launch).
+// workgroup sums the counts of the tiles before its first (all final:
+// k_search is done), then carries the base across its own, and the last tile
+// writes the batch total.  Bit 1: the records are NarrowRec (a grouped
+// launch).
 
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGroup grp, uint32_t flags) {
+    constexpr uint32_t E = kEmitTiles;
     const uint32_t fold = flags & 1u, narrow = flags & 2u;
     __shared__ P sC[kMaxSigma + 1];
-    __shared__ uint64_t s_scan[4], s_part[4];
+    __shared__ uint64_t s_scan[E][4], s_part[4];
     if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
-    const uint32_t jb = group_batch(grp, blockIdx.x);
+    const uint32_t jb = emit_batch(grp, blockIdx.x);
     const LocateBatch &B = grp.b[jb];
     const uint64_t npat = B.npat, G = (npat + 255) / 256;
-    const uint64_t g = blockIdx.x - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
+    const uint64_t g0 = (uint64_t)(blockIdx.x - grp.emit_begin[jb]) * E;
     const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
-    P lo = 0, rloc = 0;
-    uint64_t mask = 0, cnt = 0;
-    uint32_t mode = kHitOne;
-    if (i < npat)
-        cnt = narrow ? unpack_narrow<P>(reinterpret_cast<const NarrowRec<P> *>(recs)[i], lo, rloc, mask, mode)
-                     : unpack_rec<P>(recs[i], lo, rloc, mask, mode);
-    // the tile's base offset (fold: the earlier tiles' counts, summed here)
-    // and the exclusive scan of the counts, one barrier for both
+    P lo[E], rloc[E];
+    uint64_t mask[E], cnt[E];
+    uint32_t mode[E];
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint64_t i = (g0 + k) * 256u + threadIdx.x;
+        lo[k] = rloc[k] = 0;
+        mask[k] = cnt[k] = 0;
+        mode[k] = kHitOne;
+        if (i < npat)
+            cnt[k] = narrow ? unpack_narrow<P>(reinterpret_cast<const NarrowRec<P> *>(recs)[i], lo[k], rloc[k],
+                                               mask[k], mode[k])
+                            : unpack_rec<P>(recs[i], lo[k], rloc[k], mask[k], mode[k]);
+    }
+    // the first tile's base offset (fold: the earlier tiles' counts, summed
+    // here) and the exclusive scans of the counts, one barrier for all
     uint64_t part = 0;
     if (fold)
-        for (uint64_t t = threadIdx.x; t < g; t += 256) part += B.tiles[t];
+        for (uint64_t t = threadIdx.x; t < g0; t += 256) part += B.tiles[t];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t x = cnt;
+    uint64_t x[E];
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) x[k] = cnt[k];
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
+#pragma unroll
+        for (uint32_t k = 0; k < E; ++k) {
+            const uint64_t y = __shfl_up(x[k], d);
+            if (lane >= d) x[k] += y;
+        }
         part += __shfl_xor(part, d);
     }
-    if (lane == 63) { s_scan[wv] = x; s_part[wv] = part; }
-    __syncthreads();  // (also publishes sC)
-    uint64_t before = 0, agg = 0, base = fold ? 0 : B.tiles[G + g];
+    if (lane == 63) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        if (w < wv) before += s_scan[w];
-        agg += s_scan[w];
-        if (fold) base += s_part[w];
+        for (uint32_t k = 0; k < E; ++k) s_scan[k][wv] = x[k];
+        s_part[wv] = part;
     }
-    const uint64_t my_off = base + before + x - cnt;
-    if (fold && g == G - 1 && threadIdx.x == 0) {
-        B.loc_off[npat] = base + agg;
-        *B.needed = base + agg;
-    }
-    if (i < npat) B.loc_off[i] = my_off;
+    __syncthreads();  // (also publishes sC)
+    uint64_t base = fold ? s_part[0] + s_part[1] + s_part[2] + s_part[3] : 0;
     if (grp.tile_ctr && blockIdx.x == 0 && threadIdx.x == 0) *grp.tile_ctr = 0u;  // (k_search is done with it)
-    emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, B.cap,
-                                  reinterpret_cast<P *>(B.out_locs));
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint64_t g = g0 + k;
+        if (g >= G) break;  // (workgroup-uniform)
+        uint64_t before = 0, agg = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            if (w < wv) before += s_scan[k][w];
+            agg += s_scan[k][w];
+        }
+        const uint64_t tb = fold ? base : B.tiles[G + g];
+        const uint64_t my_off = tb + before + x[k] - cnt[k], i = g * 256u + threadIdx.x;
+        if (fold && g == G - 1 && threadIdx.x == 0) {
+            B.loc_off[npat] = tb + agg;
+            *B.needed = tb + agg;
+        }
+        if (i < npat) B.loc_off[i] = my_off;
+        emit_locations<P, N, VB, REC>(a, sC, my_off, cnt[k], lo[k], rloc[k], mask[k], mode[k], B.cap,
+                                      reinterpret_cast<P *>(B.out_locs));
+        base = tb + agg;
+    }
 }
 
 // Level j -> j+1: child string cS has code digit(c)*S^j + code(S); its

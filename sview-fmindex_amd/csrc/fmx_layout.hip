@@ -110,7 +110,7 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 }
 
 [[maybe_unused]] hipError_t op_search_grouped(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
-                                              uint64_t total, uint32_t cap, uint32_t pair, uint32_t xcd,
+                                              uint64_t total, uint32_t cap, uint32_t pair, uint32_t opts,
                                               hipStream_t s) {
     return disp(vb, rec, [&]<int VB, int R>() {
         const uint32_t per = pair ? 512u : 256u;
@@ -118,10 +118,11 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
         if (grid == 0 || grid > 0x7FFFFFFFull || cap == 0 || cap > kGroupRawStage) return hipErrorInvalidValue;
         if (pair)
             hipLaunchKernelGGL((k_search_grouped<P, N, VB, R, 2>), dim3((uint32_t)grid), dim3(256),
-                               512 * cap + qa.kt_lds_bytes, s, qa, grp, total, cap, xcd);
+                               grouped_pat_bytes(2, cap, 0) + qa.kt_lds_bytes, s, qa, grp, total, cap, opts & 0xffu);
         else
             hipLaunchKernelGGL((k_search_grouped<P, N, VB, R, 1>), dim3((uint32_t)grid), dim3(256),
-                               256 * cap + qa.kt_lds_bytes, s, qa, grp, total, cap, xcd);
+                               grouped_pat_bytes(1, cap, opts >> 8) + qa.kt_lds_bytes, s, qa, grp, total, cap,
+                               opts);
         return hipGetLastError();
     });
 }

@@ -86,24 +86,34 @@ __global__ __launch_bounds__(256) void k_group_scan(uint32_t *cnt) {
 }
 
 // 4. Each tile's count (k_emit's tile offsets) and each pattern's count (the
-// optional counts output, in order here).
+// optional counts output, in order here); kEmitTiles tiles per workgroup, as
+// k_emit (every record load of a lane in flight at once).
 template <typename P>
 __global__ __launch_bounds__(256) void k_group_tiles(const LocateGroup grp) {
-    __shared__ uint64_t s_w[4];
-    const uint32_t vt = blockIdx.x, jb = group_batch(grp, vt);
+    constexpr uint32_t E = kEmitTiles;
+    __shared__ uint64_t s_w[E][4];
+    const uint32_t jb = emit_batch(grp, blockIdx.x);
     const LocateBatch &B = grp.b[jb];
-    const uint64_t G = (B.npat + 255) / 256, g = vt - grp.tile_begin[jb], i = g * 256u + threadIdx.x;
+    const uint64_t G = (B.npat + 255) / 256, g0 = (uint64_t)(blockIdx.x - grp.emit_begin[jb]) * E;
     const NarrowRec<P> *__restrict__ recs = reinterpret_cast<const NarrowRec<P> *>(B.tiles + 2 * G);
-    uint64_t cnt = 0;
-    if (i < B.npat) {
-        cnt = (uint64_t)recs[i].b;
-        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = (P)cnt;
+    uint64_t cnt[E];
+#pragma unroll
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint64_t i = (g0 + k) * 256u + threadIdx.x;
+        cnt[k] = i < B.npat ? (uint64_t)recs[i].b : 0ull;
     }
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = cnt;
+    for (uint32_t k = 0; k < E; ++k) {
+        const uint64_t i = (g0 + k) * 256u + threadIdx.x;
+        if (B.out_cnt && i < B.npat) reinterpret_cast<P *>(B.out_cnt)[i] = (P)cnt[k];
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) cnt[k] += __shfl_xor(cnt[k], d);
+        if ((threadIdx.x & 63) == 0) s_w[k][threadIdx.x >> 6] = cnt[k];
+    }
     __syncthreads();
-    if (threadIdx.x == 0) B.tiles[g] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (threadIdx.x < E && g0 + threadIdx.x < G)
+        B.tiles[g0 + threadIdx.x] = s_w[threadIdx.x][0] + s_w[threadIdx.x][1] + s_w[threadIdx.x][2] +
+                                    s_w[threadIdx.x][3];
 }
 
 // ------------------------------------------- grouped launches: debug check
@@ -330,8 +340,9 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
 
 // A grouped launch's search (kWsHeader): key counts, their scan, the sorted
 // order, the search in key order, tile counts.
-static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
+static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t ewg,
                                         uint64_t total, uint32_t sb, uint32_t bits, bool raw, hipStream_t stream) {
+    const uint32_t tiles = grp.tile_begin[grp.n - 1] + (uint32_t)((grp.b[grp.n - 1].npat + 255) / 256);
     const Disp d = dispatch(ix);
     grp.gcount = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader + 256);
     grp.gkey_len = ix->gkey_len;
@@ -394,14 +405,21 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
     if (raw && cap > kGroupRawStage) cap = 4;
     // (two patterns per lane: packed records only — 512 lanes' staging would not fit LDS)
-    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair && !raw, ix->grouped_xcd,
+    // the in-workgroup sort's symbols: as many after the key as base^w <= 256 allows (none when every
+    // pattern ends within the key)
+    uint32_t wsort = 0;
+    if (ix->grouped_wsort && !raw && !(ix->grouped_pair) && maxm > grp.gkey_len)
+        for (uint32_t w = 1, p = grp.gkey_base; p <= 256 && w <= 8 && w <= maxm - grp.gkey_len; ++w, p *= grp.gkey_base)
+            wsort = w;
+    const uint32_t opts = (ix->grouped_xcd ? kGroupedXcd : 0u) | wsort << 8;
+    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair && !raw, opts,
                                    stream)) !=
         hipSuccess)
         return e;
     if (p4)
-        hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(tiles), dim3(256), 0, stream, grp);
+        hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(ewg), dim3(256), 0, stream, grp);
     else
-        hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(tiles), dim3(256), 0, stream, grp);
+        hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(ewg), dim3(256), 0, stream, grp);
     return hipGetLastError();
 }
 
@@ -426,16 +444,19 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
     const Disp d = dispatch(ix);
     LocateGroup grp = grp_in;
     uint64_t total = 0;
+    uint32_t ewg = 0;  // k_emit / k_group_tiles workgroups (kEmitTiles tiles of one batch each)
     for (uint32_t j = 0; j < grp.n; ++j) {
         grp.b[j].first = total;
         total += grp.b[j].npat;
+        grp.emit_begin[j] = ewg;
+        ewg += (uint32_t)(((grp.b[j].npat + 255) / 256 + kEmitTiles - 1) / kEmitTiles);
     }
     bool raw = false;
     const uint32_t bits = group_pack_bits(ix, grp, &raw);
     const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= (raw ? ix->grouped_raw_min : ix->grouped_min) &&
                          !grp.tile_ctr &&
                          search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
-    hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, tiles, total, sb, bits, raw, stream)
+    hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, stream)
                            : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
@@ -446,7 +467,7 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // (k_emit's flags: bit 0 fold, bit 1 NarrowRec records from the grouped search)
-    return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold | (grouped ? 2u : 0u), stream);
+    return d.ops->emit(qa, d.vb, d.rec, grp, ewg, fold | (grouped ? 2u : 0u), stream);
 }
 
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,

@@ -42,15 +42,57 @@ def gpu_build(pkg, text, sigma, pb, planes, vb, k, sr, table):
     return blob
 
 
+def diagnose(pkg, ix, load, data, offsets, pats, goff, ooff):
+    """On a count mismatch, what the failure looks like (kept in the assert
+    message): the patterns that differ, whose count they got, the count path's
+    answer for them, whether the same call differs again (three reruns on this
+    index) and the answer of a fresh index in launch order (FMX_GROUPED=0)."""
+    oc = np.diff(ooff.astype(np.int64))
+    bad = np.flatnonzero(np.diff(goff.astype(np.int64)) != oc)
+    gc = np.diff(goff.astype(np.int64))
+    out = [f"{bad.size} of {len(pats)} patterns differ"]
+    for b in bad[:6]:
+        same = sorted({pats[j] for j in np.flatnonzero(oc == gc[b])})[:3]
+        out.append(f"pat {b} {pats[b]!r}: gpu {gc[b]} oracle {oc[b]} (the oracle count of {same!r})")
+    try:
+        cnt = ix.count_batch((data, offsets)).astype(np.int64)
+        out.append(f"count path on those: {cnt[bad[:6]].tolist()}")
+        for r in range(3):
+            g2, _ = ix.locate_batch((data, offsets))
+            b2 = np.flatnonzero(np.diff(g2.astype(np.int64)) != oc)
+            out.append(f"rerun {r}: {b2.size} differ {b2[:6].tolist()}")
+        saved = os.environ.get("FMX_GROUPED")
+        os.environ["FMX_GROUPED"] = "0"
+        try:
+            ix2 = load()
+            g3, _ = ix2.locate_batch((data, offsets))
+            ix2.close()
+        finally:
+            if saved is None:
+                os.environ.pop("FMX_GROUPED", None)
+            else:
+                os.environ["FMX_GROUPED"] = saved
+        b3 = np.flatnonzero(np.diff(g3.astype(np.int64)) != oc)
+        out.append(f"fresh index, launch order: {b3.size} differ {b3[:6].tolist()}")
+    except Exception as e:  # (the diagnosis must not hide the original failure)
+        out.append(f"diagnosis stopped: {e!r}")
+    return "; ".join(out)
+
+
 def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True):
     L = O.layout(pb, planes, vb, enc)
     orc = O.OracleIndex(blob, L)
     encoder = pkg.text_encoders.EncodingTable if enc == 0 else pkg.text_encoders.PassThrough
-    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, options=occ)
+
+    def load():
+        return pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, options=occ)
+    ix = load()
     data, offsets = pkg.pack_patterns(pats)
     ooff, olocs = orc.locate_batch(data, offsets)
     goff, glocs = ix.locate_batch((data, offsets))
-    assert np.array_equal(goff, ooff), "per-pattern counts / offsets differ"
+    if not np.array_equal(goff, ooff):
+        pytest.fail("per-pattern counts / offsets differ: " + diagnose(pkg, ix, load, data, offsets, pats, goff,
+                                                                        ooff))
     assert np.array_equal(glocs, olocs), "locations differ (SA-row order)"
     cnt = ix.count_batch((data, offsets))
     assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff))

@@ -26,6 +26,7 @@ def grouped(monkeypatch):
     monkeypatch.setenv("FMX_GROUPED", "1")
     monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")  # k_group_refine on every grouped launch, however small
     monkeypatch.setenv("FMX_GROUP_CHECK", "1")  # the device-side check of the sorted order (k_group_check_*)
+    monkeypatch.setenv("FMX_DEBUG", "1")  # (an FMX_E_DEVICE names its cause on stderr)
 
 
 def pack_bits(sigma):

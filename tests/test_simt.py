@@ -322,3 +322,19 @@ def test_timing_long_region_simt(pkg, O, simt):
     assert all(t[k]["launches"] == 40 for k in ("locate", "locate.search", "locate.emit"))
     ix.timing_enable(False)
     ix.close()
+
+
+@pytest.mark.parametrize("pb,planes,vb", [(4, 2, 64), (4, 2, 32), (8, 3, 128)])
+def test_gpu_grouped_sweep_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
+    """test_gpu_grouped.py::test_every_layout_grouped's whole sweep for these
+    layouts (every alphabet size and length, forward and reversed, blob and
+    interleaved index) with the same environment: grouped, refine and the
+    device check on."""
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
+    simt.simt_config(pb * 7 + planes * 5 + vb, 0.5)
+    for sigma, m, text, table, k, sr, pats in grouped_case_inputs(pb, planes, vb):
+        blob = O.build(text, sigma, O.layout(pb, planes, vb), k, sr, table)
+        for occ in (0, 1):
+            check_simt(pkg, O, blob, pb, planes, vb, pats, occ)
