@@ -16,6 +16,7 @@
 #   refineab k_group_refine on / off, alternating twice
 #   c1ab     C1 at a 2 s and a 0.2 s timed region
 #   knobs    headline A/B: no XCD order, 3 streams, 128 x 4 streams, two patterns per lane
+#   freshreps  test_every_layout_grouped[4-2-*] in 12 fresh processes, then the grouped file 3 times (FMX_DEBUG=1)
 #   wsortab  the grouped search's in-workgroup sort by the next symbols on / off (FMX_GROUPED_WSORT=0), twice
 #   emitab   k_emit / k_group_tiles with 4 tiles per workgroup (this build) vs 1 (build_ab/libfmx_e1.so
 #            via FMX_LIB, built with -DFMX_EMIT_TILES=1), alternating twice
@@ -72,6 +73,15 @@ for step in "$@"; do
             run knob_g128_s4 300 $B --group 128 --streams 4 || exit 1
             FMX_GROUPED_PAIR=1 run knob_pair 300 $B || exit 1
             run knob_ref2 300 $B || exit 1 ;;
+        freshreps)
+            for i in 1 2 3 4 5 6 7 8 9 10 11 12; do
+                FMX_DEBUG=1 run "rep_$i" 120 python -u -m pytest tests/test_gpu_grouped.py -x -q --timeout 60 \
+                    --timeout-method thread -k "every_layout_grouped and 4-2" || exit 1
+            done
+            for i in 1 2 3; do
+                FMX_DEBUG=1 run "full_$i" 200 python -u -m pytest tests/test_gpu_grouped.py -x -q --timeout 60 \
+                    --timeout-method thread || exit 1
+            done ;;
         wsortab)
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
             for r in 1 2; do
