@@ -17,6 +17,8 @@
 #   c1ab     C1 at a 2 s and a 0.2 s timed region
 #   knobs    headline A/B: no XCD order, 3 streams, 128 x 4 streams, two patterns per lane
 #   freshreps  test_every_layout_grouped[4-2-*] in 12 fresh processes, then the grouped file 3 times (FMX_DEBUG=1)
+#   countab  the count pass decoding the key's bytes only (this build) vs the whole pattern
+#            (build_ab/libfmx_fullcount.so via FMX_LIB), alternating twice
 #   wsortab  the grouped search's in-workgroup sort by the next symbols on / off (FMX_GROUPED_WSORT=0), twice
 #   emitab   k_emit / k_group_tiles with 4 tiles per workgroup (this build) vs 1 (build_ab/libfmx_e1.so
 #            via FMX_LIB, built with -DFMX_EMIT_TILES=1), alternating twice
@@ -81,6 +83,12 @@ for step in "$@"; do
             for i in 1 2 3; do
                 FMX_DEBUG=1 run "full_$i" 200 python -u -m pytest tests/test_gpu_grouped.py -x -q --timeout 60 \
                     --timeout-method thread || exit 1
+            done ;;
+        countab)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "count_key_$r" 300 $B || exit 1
+                FMX_LIB=$PWD/build_ab/libfmx_fullcount.so run "count_full_$r" 300 $B || exit 1
             done ;;
         wsortab)
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"

@@ -466,7 +466,8 @@ __device__ __forceinline__ uint32_t lds_upper(const T *tab, uint32_t n, K x) {
 //     words holding the key's symbols are read (the pattern's last gkey_len
 //     symbols: its last bytes, or its first for reversed input), and the
 //     record carries the pattern id alone — k_search_grouped reads the
-//     pattern's bytes itself.
+//     pattern's bytes itself.  The count pass of every grouped launch runs
+//     this way (it needs the key alone).
 template <int W, bool PLACE, bool RAW = false>
 __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
     constexpr uint32_t T = 1024, PPT = kGroupChunkTiles * 256 / T;  // patterns per thread

@@ -366,14 +366,10 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     for (uint32_t j = 0; j < grp.n; ++j) maxm = std::max<uint32_t>(maxm, grp.b[j].stride);
     // (W = 6 words hold patterns up to 21 bytes at any alignment, 8 up to 29, 25 up to 97; raw: the key's
     // gkey_len <= 16 bytes in 5)
-    if (raw)
-        hipLaunchKernelGGL((k_group_key<5, false, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    else if (maxm <= 21)
-        hipLaunchKernelGGL((k_group_key<6, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    else if (maxm <= 29)
-        hipLaunchKernelGGL((k_group_key<8, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    else
-        hipLaunchKernelGGL((k_group_key<25, false>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the
+    // id-only variant's count pass, for packed records too: the decode, one LDS lookup per byte, bounds
+    // these passes, not their loads — profiles/r4/r4q_*, r4r_*)
+    hipLaunchKernelGGL((k_group_key<5, false, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);

@@ -115,8 +115,9 @@ def test_grouped_verdict_r3_case(pkg, O, simt, monkeypatch, seed):
 
 @pytest.mark.parametrize("pb,planes,vb", ALL_LAYOUTS)
 def test_every_layout_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
-    """Every layout, grouped and in launch order, blob layout and interleaved
-    records: the largest alphabet of the GPU sweep at m = k and m = 7 (the
+    """Every layout, grouped (blob layout and interleaved records), grouped
+    with id-only records and in launch order (interleaved records): the
+    largest alphabet of the GPU sweep at m = k and m = 7 (the
     smallest alphabet, whose patterns have ~800 occurrences each, runs in the
     round-3 case above)."""
     simt.simt_config(pb * 131 + planes * 17 + vb, 0.5)
@@ -127,12 +128,12 @@ def test_every_layout_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
         if not (sigma == sig[-1] and m in (k, 7)):
             continue
         blob = O.build(text, sigma, O.layout(pb, planes, vb), k, sr, table)
-        for grouped in ("1", "raw", "0"):
+        for grouped, occs in (("1", (0, 1)), ("raw", (1,)), ("0", (1,))):
             # "raw": grouped with id-only sorted records (the search reads the pattern bytes)
             monkeypatch.setenv("FMX_GROUPED", "0" if grouped == "0" else "1")
             monkeypatch.setenv("FMX_GROUPED_RAW", "1" if grouped == "raw" else "0")
-            for occ in (0, 1):
-                check_simt(pkg, O, blob, pb, planes, vb, pats[:150] + pats[-43:], occ, reversed_too=grouped != "0")
+            for occ in occs:
+                check_simt(pkg, O, blob, pb, planes, vb, pats[:110] + pats[-43:], occ, reversed_too=grouped != "0")
 
 
 def test_group_launch_garbage_workspaces_simt(pkg, O, simt, monkeypatch):
@@ -214,12 +215,12 @@ def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
     """Fault injection: the grouped launch's key
     counters are left dirty, as a launch cut short between its count pass
     and its end would leave them without the zeroing memset.
-      * -1 in key 0 (ending AAAAAA: three patterns have it) and +1 in the
-        last key: the runs of the keys between shift down by one, two
-        patterns share a sorted position and the last one is never written —
-        every position stays inside the launch, so the place pass's guard
-        passes it (no error without the check) and only FMX_GROUP_CHECK=1
-        sees it: FMX_E_DEVICE;
+      * -1 in key 1 and +1 in key 2 (patterns ending CAAAAA and GAAAAA,
+        three of each): key 2's run starts one early, two patterns share a
+        sorted position and the run's last one is never written — every
+        position stays inside the launch and every bucket total is right,
+        so the placing passes' guards pass it (no error without the check)
+        and only FMX_GROUP_CHECK=1 sees it: FMX_E_DEVICE;
       * +5 in key 0: positions run past the launch's end; the place pass's
         guard refuses them: FMX_E_DEVICE without the check.
     The index answers correctly again on the next (clean) launch."""
@@ -230,7 +231,8 @@ def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
     text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=6_000).astype(np.uint8).tobytes()
     blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
     orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
-    pats = [text[s:s + 12] for s in rng.integers(0, len(text) - 12, size=700)] + [b"CCCCCCAAAAAA"] * 3
+    pats = [text[s:s + 12] for s in rng.integers(0, len(text) - 12, size=700)]
+    pats += [b"CCCCCCAAAAAA"] * 3 + [b"CCCCCCCAAAAA"] * 3 + [b"CCCCCCGAAAAA"] * 3
     data, offsets = pkg.pack_patterns(pats)
     want = orc.locate_batch(data, offsets)
 
@@ -239,7 +241,7 @@ def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
         simt.simt_memset_fault(4 * GROUP_BINS, w, GROUP_BINS)
 
     shifted = [0] * GROUP_BINS
-    shifted[0], shifted[-1] = 0xFFFFFFFF, 1
+    shifted[1], shifted[2] = 0xFFFFFFFF, 1
     over = [0] * GROUP_BINS
     over[0] = 5
     for check, words, caught in (("1", shifted, True), ("0", shifted, False), ("0", over, True),
@@ -324,12 +326,14 @@ def test_timing_long_region_simt(pkg, O, simt):
     ix.close()
 
 
+@pytest.mark.skipif(os.environ.get("FMX_SIMT_SWEEP") != "1", reason="minutes each: FMX_SIMT_SWEEP=1")
 @pytest.mark.parametrize("pb,planes,vb", [(4, 2, 64), (4, 2, 32), (8, 3, 128)])
 def test_gpu_grouped_sweep_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
     """test_gpu_grouped.py::test_every_layout_grouped's whole sweep for these
     layouts (every alphabet size and length, forward and reversed, blob and
     interleaved index) with the same environment: grouped, refine and the
-    device check on."""
+    device check on (the layouts of the unexplained GPU failure of round 4,
+    DESIGN.md §2; opt-in, ~2 minutes each)."""
     monkeypatch.setenv("FMX_GROUPED", "1")
     monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")
     monkeypatch.setenv("FMX_GROUP_CHECK", "1")
