@@ -241,9 +241,10 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
  * at load: FMX_GROUPED=0 never, =1 always — longer patterns too, with
  * id-only records —, FMX_GROUPED_MIN=<patterns>, FMX_GROUPED_RAW=1 id-only
  * records, FMX_GROUP_REFINE_MIN=<patterns> re-sorts each key's run by the
- * next symbols, FMX_GROUP_CHECK=1 checks each launch's sorted order on the
- * device before its search — a violation is FMX_E_DEVICE; debug).  No kernel
- * makes one workgroup wait on another. */
+ * next symbols, FMX_GROUPED_WSORT=0 turns off the search's in-workgroup sort
+ * by the next symbols, FMX_GROUP_CHECK=1 checks each launch's sorted order on
+ * the device before its search — a violation is FMX_E_DEVICE; debug).  No
+ * kernel makes one workgroup wait on another. */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)

@@ -411,6 +411,51 @@ static fmx_status ensure_scratch(fmx_index *ix, uint64_t bytes) {
     return FMX_OK;
 }
 
+// Host-API copies go through a pinned stage (kStageHost bytes, allocated on
+// first use): the CPU copies between the caller's pageable buffer and the
+// stage, the DMA engine between the stage and HBM, chunk by chunk — no DMA
+// reads or writes the caller's pageable pages.  (Round 4, DESIGN.md §2: in
+// two GPU runs a few patterns were answered as if some of their bytes were
+// different, by the count path and by a fresh index alike, while the
+// caller's buffer and the oracle said otherwise.)
+constexpr uint64_t kStageHost = 8ull << 20;  // the stage grows to a copy's size up to this, then copies chunk
+static hipError_t ensure_stage(fmx_index *ix, uint64_t n) {
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n, 64 << 10), kStageHost);
+    if (ix->h_stage_bytes >= want) return hipSuccess;
+    if (ix->h_stage) hipHostFree(ix->h_stage);
+    ix->h_stage_bytes = 0;
+    hipError_t e = hipHostMalloc(&ix->h_stage, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        ix->h_stage = nullptr;
+        return e;
+    }
+    ix->h_stage_bytes = want;
+    return hipSuccess;
+}
+static hipError_t h2d_staged(fmx_index *ix, uint8_t *d, const void *h, uint64_t n, hipStream_t s) {
+    hipError_t e = hipStreamSynchronize(s);  // (the stage's earlier copies are done before it is regrown)
+    if (e == hipSuccess) e = ensure_stage(ix, n);
+    for (uint64_t o = 0; e == hipSuccess && o < n; o += ix->h_stage_bytes) {
+        const uint64_t c = std::min(n - o, ix->h_stage_bytes);
+        e = hipStreamSynchronize(s);  // (the stage's previous copy has been read)
+        if (e != hipSuccess) break;
+        memcpy(ix->h_stage, static_cast<const uint8_t *>(h) + o, c);
+        e = hipMemcpyAsync(d + o, ix->h_stage, c, hipMemcpyHostToDevice, s);
+    }
+    return e;
+}
+static hipError_t d2h_staged(fmx_index *ix, void *h, const uint8_t *d, uint64_t n, hipStream_t s) {
+    hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = ensure_stage(ix, n);
+    for (uint64_t o = 0; e == hipSuccess && o < n; o += ix->h_stage_bytes) {
+        const uint64_t c = std::min(n - o, ix->h_stage_bytes);
+        e = hipMemcpyAsync(ix->h_stage, d + o, c, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) memcpy(static_cast<uint8_t *>(h) + o, ix->h_stage, c);
+    }
+    return e;
+}
+
 static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     QueryArgs &q = ix->qa;
     const BlobView &v = ix->bv;
@@ -886,6 +931,7 @@ void fmx_free(fmx_index *ix) {
     for (auto &sl : ix->slots)
         if (sl.done) hipEventDestroy(sl.done);
     if (ix->d_scratch) hipFree(ix->d_scratch);
+    if (ix->h_stage) hipHostFree(ix->h_stage);
     if (ix->d_ws) hipFree(ix->d_ws);
     if (ix->d_occ) hipFree(ix->d_occ);
     if (ix->d_dlut) hipFree(ix->d_dlut);
@@ -1111,13 +1157,13 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     if (st) return st;
     hipStream_t s = ix->stream;
     uint8_t *d = ix->d_scratch;
-    hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
+    hipError_t e = h2d_staged(ix, d, bytes, nb, s);
+    if (e == hipSuccess) e = h2d_staged(ix, d + o_off, offsets, (n + 1) * 8, s);
     if (e != hipSuccess) return FMX_E_DEVICE;
     flags = (flags & 0xffu) | stage_hint(offsets, n);
     st = fmx_count_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, d + o_cnt, s);
     if (st) return st;
-    if (hipMemcpyAsync(out_counts, d + o_cnt, n * pb, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
+    if (d2h_staged(ix, out_counts, d + o_cnt, n * pb, s) != hipSuccess) return FMX_E_DEVICE;
     return read_status(ix, s);
 }
 
@@ -1167,28 +1213,24 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
         st = ensure_scratch(ix, o_locs + std::max<uint64_t>(dcap, 1) * pb);
         if (st) return st;
         uint8_t *d = ix->d_scratch;
-        hipError_t e = hipMemcpyAsync(d, bytes, nb, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(d + o_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s);
+        hipError_t e = h2d_staged(ix, d, bytes, nb, s);
+        if (e == hipSuccess) e = h2d_staged(ix, d + o_off, offsets, (n + 1) * 8, s);
         if (e != hipSuccess) return FMX_E_DEVICE;
         st = fmx_locate_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, (uint64_t *)(d + o_loff),
                                     d + o_locs, dcap, (uint64_t *)(d + o_need), ix->d_ws, ix->ws_bytes, s);
         if (st) return st;
         uint64_t total = 0;
-        e = hipMemcpyAsync(&total, d + o_need, 8, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return FMX_E_DEVICE;
+        if (d2h_staged(ix, &total, d + o_need, 8, s) != hipSuccess) return FMX_E_DEVICE;
         st = read_status(ix, s);
         if (st) return st;
         if (needed) *needed = total;
         if (total > cap) {
-            if (hipMemcpy(out_loc_offsets, d + o_loff, (n + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess)
-                return FMX_E_DEVICE;
+            if (d2h_staged(ix, out_loc_offsets, d + o_loff, (n + 1) * 8, s) != hipSuccess) return FMX_E_DEVICE;
             return FMX_E_CAPACITY;
         }
         if (total <= dcap) {
-            e = hipMemcpyAsync(out_loc_offsets, d + o_loff, (n + 1) * 8, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess && total) e = hipMemcpyAsync(out_locs, d + o_locs, total * pb, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            e = d2h_staged(ix, out_loc_offsets, d + o_loff, (n + 1) * 8, s);
+            if (e == hipSuccess && total) e = d2h_staged(ix, out_locs, d + o_locs, total * pb, s);
             return dev_err(e);
         }
         dcap = total;  // second pass with room for every location

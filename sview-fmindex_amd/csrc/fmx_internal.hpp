@@ -190,6 +190,10 @@ struct fmx_index {
     // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
+    // pinned host staging of the host-API calls (fmx_count_batch / fmx_locate_batch): the caller's
+    // pageable buffers are only ever memcpy'd by the CPU; the DMA engine reads and writes this
+    uint8_t *h_stage = nullptr;
+    uint64_t h_stage_bytes = 0;
     uint8_t *d_ws = nullptr;
     uint64_t ws_bytes = 0;
     // timing
@@ -293,6 +297,7 @@ constexpr uint32_t kEmitTiles = FMX_EMIT_TILES;
 constexpr uint32_t kGroupKeyBits = FMX_GROUP_KEY_BITS;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;
 constexpr uint32_t kGroupChunkTiles = 16;   // tiles (of 256 patterns) per key / place workgroup
+constexpr uint32_t kCountChunks = 4;        // chunks per count-pass workgroup
 constexpr uint32_t kGroupPackBits = 96;
 constexpr uint32_t kGroupedXcd = 1;  // k_search_grouped opts: deal the key order out XCD by XCD
 constexpr uint32_t kWsortBytes = 1024 + 256 * 16;  // its in-workgroup sort's LDS (256 counters, 256 records)

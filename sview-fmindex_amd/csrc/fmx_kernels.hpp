@@ -493,16 +493,34 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     }
     for (uint32_t x = t; x < kGroupBins; x += T) hist[x] = 0;
     __syncthreads();
-    const uint32_t c = blockIdx.x, jb = group_chunk_batch(grp, c);
+    // the count pass takes kCountChunks chunks per workgroup (one set of
+    // global adds for all of them: device-scope atomics run at ~1.3 TB/s of
+    // added bytes chip-wide, MI355X_MICROARCH.md), the place pass one
+    constexpr uint32_t CPW = PLACE ? 1u : kCountChunks;
+    uint32_t key_r[PPT], rank_r[PPT];
+    U4 rec_r[PLACE ? PPT : 1];
+    uint64_t pfirst = 0, pn = 0;  // (the place pass's one chunk, after the loop)
+#pragma unroll
+    for (uint32_t r = 0; r < CPW; ++r) {
+    const uint32_t c = blockIdx.x * CPW + r;
+    if constexpr (!PLACE) {
+        const uint32_t nchunks = grp.chunk_begin[grp.n - 1] +
+                                 (uint32_t)(((grp.b[grp.n - 1].npat + 255) / 256 + kGroupChunkTiles - 1) /
+                                            kGroupChunkTiles);
+        if (c >= nchunks) break;  // (workgroup-uniform)
+    }
+    const uint32_t jb = group_chunk_batch(grp, c);
     const LocateBatch &B = grp.b[jb];
     const uint64_t n = B.npat, first = (uint64_t)(c - grp.chunk_begin[jb]) * kGroupChunkTiles * 256u;
     const uint32_t m = B.stride, bits = grp.gbits, sym_max = a.sigma, L = grp.gkey_len;
     const bool rev = B.rev != 0;
+    if constexpr (PLACE) {
+        pfirst = first;
+        pn = n;
+    }
     if (!PLACE && first == 0 && t == 0 && B.offs[0] != 0) atomicOr(a.status, kStatusStride);
     // G patterns' words in flight at once (all of a thread's when they are short)
     constexpr uint32_t G = W <= 8 ? PPT : 1;
-    uint32_t key_r[PPT], rank_r[PPT];
-    U4 rec_r[PLACE ? PPT : 1];
 #pragma unroll
     for (uint32_t p0 = 0; p0 < PPT; p0 += G) {
     uint32_t x[G][W], lead[G];
@@ -563,6 +581,7 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
         }
     }
     }
+    }
     __syncthreads();
     constexpr uint32_t per = kGroupBins / T;
     if constexpr (!PLACE) {
@@ -585,8 +604,8 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
         __syncthreads();
 #pragma unroll
         for (uint32_t p = 0; p < PPT; ++p) {
-            const uint64_t i = first + p * T + t;
-            if (i >= n) continue;
+            const uint64_t i = pfirst + p * T + t;
+            if (i >= pn) continue;
             const uint64_t sp = (uint64_t)hist[key_r[p]] + rank_r[p];
             if (sp >= grp.gtotal) {  // (counters not zero at entry: never write outside the sorted order)
                 atomicOr(a.status, kStatusGroup);

@@ -369,7 +369,8 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the
     // id-only variant's count pass, for packed records too: the decode, one LDS lookup per byte, bounds
     // these passes, not their loads — profiles/r4/r4q_*, r4r_*)
-    hipLaunchKernelGGL((k_group_key<5, false, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    hipLaunchKernelGGL((k_group_key<5, false, true>), dim3((chunks + kCountChunks - 1) / kCountChunks), dim3(1024), 0,
+                       stream, qa, grp, rb);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);

@@ -55,6 +55,12 @@ def diagnose(pkg, ix, load, data, offsets, pats, goff, ooff):
         same = sorted({pats[j] for j in np.flatnonzero(oc == gc[b])})[:3]
         out.append(f"pat {b} {pats[b]!r}: gpu {gc[b]} oracle {oc[b]} (the oracle count of {same!r})")
     try:
+        d2, o2 = pkg.pack_patterns(pats)
+        if not (np.array_equal(d2, data) and np.array_equal(o2, offsets)):
+            diff = np.flatnonzero(d2 != data)
+            out.append(f"the caller's pattern buffer changed since packing at bytes {diff[:8].tolist()}")
+        c2 = ix.count_batch((d2.copy(), o2.copy())).astype(np.int64)
+        out.append(f"count path on a fresh copy: {np.flatnonzero(c2 != oc).size} differ")
         cnt = ix.count_batch((data, offsets)).astype(np.int64)
         out.append(f"count path on those: {cnt[bad[:6]].tolist()}")
         for r in range(3):
