@@ -494,8 +494,8 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     for (uint32_t x = t; x < kGroupBins; x += T) hist[x] = 0;
     __syncthreads();
     // the count pass takes kCountChunks chunks per workgroup (one set of
-    // global adds for all of them: device-scope atomics run at ~1.3 TB/s of
-    // added bytes chip-wide, MI355X_MICROARCH.md), the place pass one
+    // global adds for all of them; measured no faster than one, r4w: the
+    // atomics do not bound it), the place pass one
     constexpr uint32_t CPW = PLACE ? 1u : kCountChunks;
     uint32_t key_r[PPT], rank_r[PPT];
     U4 rec_r[PLACE ? PPT : 1];
