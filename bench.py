@@ -561,7 +561,8 @@ def main():
     d_blob = torch.empty(blob_len, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     t1 = time.time()
-    bcast = dist_on and world > 1 and args.blob_source == "broadcast"
+    # (one rank with FMX_BENCH_DIST=1: the broadcast runs too — a self-broadcast that drives the RCCL path)
+    bcast = dist_on and args.blob_source == "broadcast"
     if rank == 0 or not bcast:
         builder.build_device(d_text.data_ptr(), d_blob.data_ptr(), blob_len, device=gpu)
     torch.cuda.synchronize()
@@ -626,7 +627,7 @@ def main():
     else:
         w = Workload(torch, ix, d_text, m, weak_starts(NB), P, S, GR, fixed, dev)
         if args.presorted or args.xcd_partitioned:
-            arrange(torch, w, B, m, GR, dev, args.presorted, args.presort_symbols)
+            arrange(torch, w, B, m, GR, dev, args.presorted, args.presort_symbols, cfg["alphabet"])
         steps = args.steps or 800
         launches = -(-steps // GR)
     torch.cuda.synchronize()
@@ -644,7 +645,7 @@ def main():
         needs = w.check_capacity()
         all_needs = D.all_gather_ints(needs, device=dev)
         sizes = plan.sizes() if strong else np.full((world, len(w.batches)), B, dtype=np.int64)
-        jg = D.JobGather(sizes, all_needs, GR, rank, pdt_t, dev)
+        jg = D.JobGather(sizes, all_needs, GR, rank, pdt_t, dev, collective=dist_on)
         w.rebind([(jg.counts_slot(k), jg.locs_slot(k)) for k in range(len(w.batches))])
 
     # ---- timed region: compute ----------------------------------------------
@@ -862,6 +863,14 @@ def main():
         # end from a host-resident blob: upload + load + locate
         "readme_workload_s": None if upload_s is None else upload_s + load_s + 100_000 / per_gpu,
         "gather": gather,
+        # what this rank holds in HBM (distributed.hbm_per_rank: the same accounting tests/test_distributed.py
+        # checks for 8 ranks against 288 GB), beside torch's measured peak (+ the index's own allocations)
+        "hbm_per_rank": dict(D.hbm_per_rank(blob=blob_len, records=info["device_bytes"], text=n,
+                                            batch_sizes=[bt["n"] for bt in w.batches], m=m, pos_bytes=P,
+                                            world=world, group=GR, loc_cap=[bt["cap"] for bt in w.batches],
+                                            gather=jg is not None and jg.collective),
+                             measured_torch_peak=int(torch.cuda.max_memory_allocated(dev)),
+                             measured_index=int(info["device_bytes"])),
         "blob_replication": replicate if replicate else
         {"how": "each rank builds the blob from the same seeded text" if world > 1 else "one rank"},
         "profile_key": key,
@@ -1072,21 +1081,23 @@ def single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, seed, min_sec
     return out
 
 
-def arrange(torch, w, B, m, GR, dev, presorted, key_symbols=14):
+def arrange(torch, w, B, m, GR, dev, presorted, key_symbols=14, alphabet=b"ACGT"):
     """Experiments (weak configs, uniform batches): rearrange each launch
-    group's patterns — sorted by reversed suffix (`presorted`), or so that
+    group's patterns — sorted by reversed suffix (`presorted`: the last
+    key_symbols symbols, digits over the text's alphabet), or so that
     workgroup tile t holds class-(t % 8) patterns (XCD-partitioned)."""
     if presorted:
         code = torch.zeros(256, dtype=torch.int64, device=dev)
-        for i, c in enumerate(b"ACGT"):
+        for i, c in enumerate(alphabet):
             code[c] = i
+        base = len(alphabet)
         for g in range(w.n_groups):
             sel = w.batches[g * GR:(g + 1) * GR]
             st = torch.cat([b["starts"] for b in sel])
             pats = torch.stack([b["pat"].view(B, m) for b in sel]).view(-1, m).long()
             key = torch.zeros(st.numel(), dtype=torch.int64, device=dev)
-            for q in range(min(m, key_symbols)):
-                key = key * 4 + code[pats[:, m - 1 - q]]
+            for q in range(min(m, key_symbols, int(62 / math.log2(base)))):
+                key = key * base + code[pats[:, m - 1 - q]]
             order = torch.argsort(key, stable=True)
             st, pats = st[order], pats[order].to(torch.uint8)
             for j, b in enumerate(sel):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 5u
+#define FMX_ABI_VERSION 6u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -142,6 +142,10 @@ typedef struct fmx_index_info {
     uint32_t group_key_base; /* ... as digits over this many symbols               */
     uint64_t grouped_min;    /* fixed-length launches of at least this many
                                 patterns are grouped (UINT64_MAX: never)            */
+    uint64_t launches_grouped;      /* locate launches of this index so far, by the
+                                       path they took: grouped with packed records, */
+    uint64_t launches_grouped_raw;  /* grouped with id-only records,                  */
+    uint64_t launches_ordered;      /* in launch order (k_search)                     */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {
@@ -228,6 +232,8 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
  * [256 B][16 KiB of key counters][tile counts][tile offsets][one search
  * record per pattern][to 16 B][one 16-B sorted-order record per pattern].
+ * The workspace must be 16-byte aligned (FMX_E_ARG otherwise: the grouped
+ * passes read and write it as 16-B vectors; hipMalloc gives 256-B alignment).
  * A workspace needs no initialisation (a grouped launch zeroes its key
  * counters on its stream first; only the FMX_SEARCH_PERSISTENT=1 A/B variant
  * wants its first 4 bytes zero) and belongs to this index: its launches are

@@ -8,6 +8,7 @@
 #   single   bench.py --single-batch only (one 100k batch per call)
 #   trace    rocprofv3 --kernel-trace --stats on bench.py --streams 1 and on the default command
 #   pmc      rocprofv3 PMC passes (FETCH/WRITE size, memory-side requests) on bench.py --streams 1
+#            (PMC_CONFIG=c4 / c5 / ...: that config instead of the default c2)
 #   configs  bench.py --config c1 / c3 / c4 / c5
 #   cli      bench_cli.py: generate, build, locate warm / cold / O_DIRECT (the README workload)
 #   c5ab     C5 grouped at 16 per launch (whole job verified) and in launch order
@@ -113,7 +114,7 @@ for step in "$@"; do
             run trace_default 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace2" -o run --output-format csv -- \
                 python3 -u bench.py --no-cpu || exit 1 ;;
         pmc)
-            P="--streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+            P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
             run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \
                 --output-format csv -- python3 -u bench.py $P || exit 1
             run pmc_ea 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \

@@ -54,7 +54,9 @@ class fmx_index_info(C.Structure):
                 ("options", C.c_uint32), ("deep_lut_k", C.c_uint32), ("device", C.c_int32),
                 ("context_len", C.c_uint32), ("scan_rows", C.c_uint32),
                 ("occ_record", C.c_uint32), ("group_key_len", C.c_uint32),
-                ("group_key_base", C.c_uint32), ("grouped_min", C.c_uint64)]
+                ("group_key_base", C.c_uint32), ("grouped_min", C.c_uint64),
+                ("launches_grouped", C.c_uint64), ("launches_grouped_raw", C.c_uint64),
+                ("launches_ordered", C.c_uint64)]
 
 
 class fmx_locate_job(C.Structure):

@@ -211,13 +211,20 @@ static void fold_span(fmx_index *ix, const TimedSpan &sp) {
     if (sp.m) ix->event_pool.push_back(sp.m);
 }
 
-// Fold the oldest spans that have completed while more than kTimedKeep are
-// pending (caller holds timing_mu).
+// While more than kTimedKeep spans are pending, fold every completed one
+// among the oldest 2 kTimedKeep — whatever stream it was on: a slow stream's
+// span at the front does not hold back the finished spans of the others
+// (caller holds timing_mu).
 static void harvest_spans(fmx_index *ix) {
-    while (ix->spans.size() > kTimedKeep && hipEventQuery(ix->spans.front().b) == hipSuccess) {
-        fold_span(ix, ix->spans.front());
-        ix->spans.pop_front();
+    if (ix->spans.size() <= kTimedKeep) return;
+    const size_t look = std::min(ix->spans.size(), 2 * kTimedKeep);
+    size_t keep = 0;
+    for (size_t i = 0; i < look; ++i) {
+        const TimedSpan sp = ix->spans[i];
+        if (hipEventQuery(sp.b) == hipSuccess) fold_span(ix, sp);
+        else ix->spans[keep++] = sp;
     }
+    ix->spans.erase(ix->spans.begin() + keep, ix->spans.begin() + look);
 }
 
 // Bracket one launch with events on its stream when timing is on.
@@ -411,48 +418,128 @@ static fmx_status ensure_scratch(fmx_index *ix, uint64_t bytes) {
     return FMX_OK;
 }
 
-// Host-API copies go through a pinned stage (kStageHost bytes, allocated on
-// first use): the CPU copies between the caller's pageable buffer and the
-// stage, the DMA engine between the stage and HBM, chunk by chunk — no DMA
-// reads or writes the caller's pageable pages.  (Round 4, DESIGN.md §2: in
-// two GPU runs a few patterns were answered as if some of their bytes were
-// different, by the count path and by a fresh index alike, while the
-// caller's buffer and the oracle said otherwise.)
-constexpr uint64_t kStageHost = 8ull << 20;  // the stage grows to a copy's size up to this, then copies chunk
-static hipError_t ensure_stage(fmx_index *ix, uint64_t n) {
-    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n, 64 << 10), kStageHost);
-    if (ix->h_stage_bytes >= want) return hipSuccess;
-    if (ix->h_stage) hipHostFree(ix->h_stage);
-    ix->h_stage_bytes = 0;
-    hipError_t e = hipHostMalloc(&ix->h_stage, want, hipHostMallocDefault);
-    if (e != hipSuccess) {
-        ix->h_stage = nullptr;
-        return e;
+// ----------------------------------------------------------------- Stage
+// (fmx_internal.hpp).  Chunks of up to max_chunk_ bytes alternate between the
+// two pinned buffers; the CPU copy of a large chunk is split over a few
+// threads (one thread copies ~10 GB/s: a 2.7 GB blob would otherwise be
+// bound by it).
+
+static void host_copy(void *dst, const void *src, uint64_t n) {
+    constexpr uint64_t kPar = 8ull << 20;  // below this, one thread
+    if (n < kPar) {
+        memcpy(dst, src, n);
+        return;
     }
-    ix->h_stage_bytes = want;
+    const unsigned nt = (unsigned)std::min<uint64_t>(4, n / (kPar / 2));
+    const uint64_t part = (n / nt + 4095) & ~4095ull;
+    std::vector<std::thread> th;
+    uint64_t o = part;
+    try {  // (no exception may leave the C ABI)
+        for (; o < n; o += part)
+            th.emplace_back([=] { memcpy((uint8_t *)dst + o, (const uint8_t *)src + o, std::min(part, n - o)); });
+    } catch (...) {
+        for (; o < n; o += part) memcpy((uint8_t *)dst + o, (const uint8_t *)src + o, std::min(part, n - o));
+    }
+    memcpy(dst, src, std::min(part, n));
+    for (auto &t : th) t.join();
+}
+
+Stage::~Stage() {
+    drain();
+    for (int b = 0; b < 2; ++b) {
+        if (ev_[b]) hipEventDestroy(ev_[b]);
+        if (buf_[b]) hipHostFree(buf_[b]);
+    }
+}
+
+hipError_t Stage::wait(int b) {
+    if (!pending_[b]) return hipSuccess;
+    const hipError_t e = hipEventSynchronize(ev_[b]);
+    if (e == hipSuccess) pending_[b] = false;
+    return e;
+}
+
+hipError_t Stage::drain() {
+    hipError_t e = wait(0);
+    const hipError_t e1 = wait(1);
+    return e != hipSuccess ? e : e1;
+}
+
+// Buffers of min(max(n, 64 KiB), max_chunk_) bytes (regrown only once both
+// are idle).
+hipError_t Stage::reserve(uint64_t n) {
+    uint64_t cap = max_chunk_;
+    if (const char *e = getenv("FMX_STAGE_CHUNK")) {  // (tests: small chunks exercise the double buffering)
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v >= 64) cap = std::min(cap, v);
+    }
+    const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(n, 64 << 10), cap);
+    if (!ev_[0] || !ev_[1]) {
+        for (int b = 0; b < 2; ++b)
+            if (!ev_[b]) {
+                const hipError_t e = hipEventCreateWithFlags(&ev_[b], hipEventDisableTiming);
+                if (e != hipSuccess) { ev_[b] = nullptr; return e; }
+            }
+    }
+    if (chunk_ >= want) return hipSuccess;
+    hipError_t e = drain();
+    if (e != hipSuccess) return e;
+    for (int b = 0; b < 2; ++b) {
+        if (buf_[b]) hipHostFree(buf_[b]);
+        buf_[b] = nullptr;
+    }
+    chunk_ = 0;
+    for (int b = 0; b < 2; ++b)
+        if ((e = hipHostMalloc(&buf_[b], want, hipHostMallocDefault)) != hipSuccess) {
+            buf_[b] = nullptr;
+            return e;
+        }
+    chunk_ = want;
     return hipSuccess;
 }
-static hipError_t h2d_staged(fmx_index *ix, uint8_t *d, const void *h, uint64_t n, hipStream_t s) {
-    hipError_t e = hipStreamSynchronize(s);  // (the stage's earlier copies are done before it is regrown)
-    if (e == hipSuccess) e = ensure_stage(ix, n);
-    for (uint64_t o = 0; e == hipSuccess && o < n; o += ix->h_stage_bytes) {
-        const uint64_t c = std::min(n - o, ix->h_stage_bytes);
-        e = hipStreamSynchronize(s);  // (the stage's previous copy has been read)
-        if (e != hipSuccess) break;
-        memcpy(ix->h_stage, static_cast<const uint8_t *>(h) + o, c);
-        e = hipMemcpyAsync(d + o, ix->h_stage, c, hipMemcpyHostToDevice, s);
+
+hipError_t Stage::h2d(void *d, const void *h, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    std::lock_guard<std::mutex> g(mu_);
+    hipError_t e = reserve(n);
+    for (uint64_t o = 0; e == hipSuccess && o < n; o += chunk_) {
+        const uint64_t c = std::min(n - o, chunk_);
+        const int b = next_;
+        next_ ^= 1;
+        if ((e = wait(b)) != hipSuccess) break;  // (the buffer's previous copy has read it)
+        host_copy(buf_[b], static_cast<const uint8_t *>(h) + o, c);
+        e = hipMemcpyAsync(static_cast<uint8_t *>(d) + o, buf_[b], c, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipEventRecord(ev_[b], s);
+        if (e == hipSuccess) pending_[b] = true;
     }
     return e;
 }
-static hipError_t d2h_staged(fmx_index *ix, void *h, const uint8_t *d, uint64_t n, hipStream_t s) {
-    hipError_t e = hipStreamSynchronize(s);
-    if (e == hipSuccess) e = ensure_stage(ix, n);
-    for (uint64_t o = 0; e == hipSuccess && o < n; o += ix->h_stage_bytes) {
-        const uint64_t c = std::min(n - o, ix->h_stage_bytes);
-        e = hipMemcpyAsync(ix->h_stage, d + o, c, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e == hipSuccess) memcpy(static_cast<uint8_t *>(h) + o, ix->h_stage, c);
+
+hipError_t Stage::d2h(void *h, const void *d, uint64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    std::lock_guard<std::mutex> g(mu_);
+    hipError_t e = reserve(n);
+    if (e == hipSuccess) e = drain();  // (both buffers free: an earlier h2d may still be reading them)
+    const uint64_t chunks = e == hipSuccess ? (n + chunk_ - 1) / chunk_ : 0;
+    // chunk i goes to buffer i & 1: the DMA of chunk i + 1 is queued before
+    // the CPU copies chunk i out
+    auto issue = [&](uint64_t i) {
+        const uint64_t o = i * chunk_, c = std::min(n - o, chunk_);
+        const int b = (int)(i & 1);
+        hipError_t x = hipMemcpyAsync(buf_[b], static_cast<const uint8_t *>(d) + o, c, hipMemcpyDeviceToHost, s);
+        if (x == hipSuccess) x = hipEventRecord(ev_[b], s);
+        if (x == hipSuccess) pending_[b] = true;
+        return x;
+    };
+    if (chunks) e = issue(0);
+    for (uint64_t i = 0; e == hipSuccess && i < chunks; ++i) {
+        if (i + 1 < chunks && (e = issue(i + 1)) != hipSuccess) break;
+        const int b = (int)(i & 1);
+        if ((e = wait(b)) != hipSuccess) break;
+        const uint64_t o = i * chunk_;
+        host_copy(static_cast<uint8_t *>(h) + o, buf_[b], std::min(n - o, chunk_));
     }
+    next_ = 0;
     return e;
 }
 
@@ -647,8 +734,9 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
     if (idx < 0) return dev_err(hipStreamSynchronize(s));  // never launched on: nothing latched
     uint32_t *w = ix->d_status + idx;
     uint32_t st = 0;
-    if (hipMemcpyAsync(&st, w, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return FMX_E_DEVICE;
-    if (hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
+    // (through the pinned stage: no DMA into this stack word; d2h returns
+    // once the word is here, so every launch queued on s before has finished)
+    if (ix->stage.d2h(&st, w, 4, s) != hipSuccess) return FMX_E_DEVICE;
     if (st) {
         // ordered on s after every launch that could have set it: nothing is lost
         if (hipMemsetAsync(w, 0, 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
@@ -734,12 +822,20 @@ fmx_status fmx_load(const uint8_t *blob, uint64_t blob_len, fmx_layout layout, i
     // record re-layout reads the blob) run on this non-blocking stream, which
     // is not ordered after the null stream — they could read the allocation's
     // previous contents (intermittent wrong counts with
-    // interleaved records only; reproduced by tests/test_simt.py)
-    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMemcpyAsync(ix->d_blob_owned, blob, blob_len, hipMemcpyHostToDevice, ix->stream) != hipSuccess ||
-        hipStreamSynchronize(ix->stream) != hipSuccess) {
+    // interleaved records only; reproduced by tests/test_simt.py).  Through a
+    // pinned stage of its own (32 MiB chunks, freed after the load): no DMA
+    // reads the caller's pageable blob (round 4).
+    if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
         fmx_free(ix);
         return FMX_E_DEVICE;
+    }
+    {
+        Stage up(32ull << 20);
+        if (up.h2d(ix->d_blob_owned, blob, blob_len, ix->stream) != hipSuccess ||
+            hipStreamSynchronize(ix->stream) != hipSuccess) {
+            fmx_free(ix);
+            return FMX_E_DEVICE;
+        }
     }
     tr.mark("host -> HBM");
     ix->d_blob = ix->d_blob_owned;
@@ -760,9 +856,10 @@ fmx_status fmx_load_device(const uint8_t *d_blob, uint64_t blob_len, fmx_layout 
     if (!dg.ok) return FMX_E_DEVICE;
     if (hipDeviceSynchronize() != hipSuccess) return FMX_E_DEVICE;  // the blob's writers, on any stream
     BlobView bv;
+    Stage hdr(64 << 10);  // the header reads land in pinned memory, then in the parser's locals
     BlobReader rd = [&](uint64_t off, uint64_t len, void *dst) {
         if (off + len > blob_len) return false;
-        return hipMemcpy(dst, d_blob + off, len, hipMemcpyDeviceToHost) == hipSuccess;
+        return hdr.d2h(dst, d_blob + off, len, nullptr) == hipSuccess;
     };
     fmx_status st = parse_blob(rd, blob_len, layout, &bv, expected_total, actual_total);
     if (st) return st;
@@ -931,7 +1028,6 @@ void fmx_free(fmx_index *ix) {
     for (auto &sl : ix->slots)
         if (sl.done) hipEventDestroy(sl.done);
     if (ix->d_scratch) hipFree(ix->d_scratch);
-    if (ix->h_stage) hipHostFree(ix->h_stage);
     if (ix->d_ws) hipFree(ix->d_ws);
     if (ix->d_occ) hipFree(ix->d_occ);
     if (ix->d_dlut) hipFree(ix->d_dlut);
@@ -970,6 +1066,9 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->group_key_len = faithful ? ix->gkey_len : 0;
     o->group_key_base = faithful ? ix->gkey_base : 0;
     o->grouped_min = faithful && ix->gkey_len ? ix->grouped_min : ~0ull;
+    o->launches_grouped = ix->launches_grouped.load();
+    o->launches_grouped_raw = ix->launches_grouped_raw.load();
+    o->launches_ordered = ix->launches_ordered.load();
     o->device = ix->device;
     return FMX_OK;
 }
@@ -1006,6 +1105,7 @@ fmx_status fmx_locate_batch_async(fmx_index *ix, const uint8_t *d_bytes, const u
                                   uint64_t cap, uint64_t *d_needed, void *d_ws, uint64_t ws_bytes, void *stream) {
     if (!ix || !d_loc_offsets || !d_needed || (n && (!d_bytes || !d_offsets)) || (cap && !d_locs)) return FMX_E_ARG;
     if (!d_ws || ws_bytes < kWsHeader + 16) return FMX_E_ARG;
+    if (((uintptr_t)d_ws & 15) != 0) return FMX_E_ARG;  // (the grouped passes' 16-B vectors: fmx.h)
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
     DeviceGuard dg(ix->device);
     if (n == 0) {
@@ -1043,7 +1143,7 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
         const fmx_locate_job &j = jobs[i];
         if (!j.d_loc_offsets || !j.d_needed || (j.n_patterns && (!j.d_bytes || !j.d_offsets)) ||
             (j.cap && !j.d_locs) || !j.d_workspace || j.workspace_bytes < ws_bytes_for(ix, j.n_patterns) ||
-            j.reserved != 0)
+            ((uintptr_t)j.d_workspace & 15) != 0 || j.reserved != 0)
             return FMX_E_ARG;
         for (uint64_t k = 0; k < i; ++k)
             if (jobs[k].d_workspace == j.d_workspace) return FMX_E_ARG;  // the batches run concurrently
@@ -1157,13 +1257,13 @@ fmx_status fmx_count_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t *
     if (st) return st;
     hipStream_t s = ix->stream;
     uint8_t *d = ix->d_scratch;
-    hipError_t e = h2d_staged(ix, d, bytes, nb, s);
-    if (e == hipSuccess) e = h2d_staged(ix, d + o_off, offsets, (n + 1) * 8, s);
+    hipError_t e = ix->stage.h2d(d, bytes, nb, s);
+    if (e == hipSuccess) e = ix->stage.h2d(d + o_off, offsets, (n + 1) * 8, s);
     if (e != hipSuccess) return FMX_E_DEVICE;
     flags = (flags & 0xffu) | stage_hint(offsets, n);
     st = fmx_count_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, d + o_cnt, s);
     if (st) return st;
-    if (d2h_staged(ix, out_counts, d + o_cnt, n * pb, s) != hipSuccess) return FMX_E_DEVICE;
+    if (ix->stage.d2h(out_counts, d + o_cnt, n * pb, s) != hipSuccess) return FMX_E_DEVICE;
     return read_status(ix, s);
 }
 
@@ -1213,24 +1313,24 @@ fmx_status fmx_locate_batch(fmx_index *ix, const uint8_t *bytes, const uint64_t 
         st = ensure_scratch(ix, o_locs + std::max<uint64_t>(dcap, 1) * pb);
         if (st) return st;
         uint8_t *d = ix->d_scratch;
-        hipError_t e = h2d_staged(ix, d, bytes, nb, s);
-        if (e == hipSuccess) e = h2d_staged(ix, d + o_off, offsets, (n + 1) * 8, s);
+        hipError_t e = ix->stage.h2d(d, bytes, nb, s);
+        if (e == hipSuccess) e = ix->stage.h2d(d + o_off, offsets, (n + 1) * 8, s);
         if (e != hipSuccess) return FMX_E_DEVICE;
         st = fmx_locate_batch_async(ix, d, (uint64_t *)(d + o_off), n, flags, nullptr, (uint64_t *)(d + o_loff),
                                     d + o_locs, dcap, (uint64_t *)(d + o_need), ix->d_ws, ix->ws_bytes, s);
         if (st) return st;
         uint64_t total = 0;
-        if (d2h_staged(ix, &total, d + o_need, 8, s) != hipSuccess) return FMX_E_DEVICE;
+        if (ix->stage.d2h(&total, d + o_need, 8, s) != hipSuccess) return FMX_E_DEVICE;
         st = read_status(ix, s);
         if (st) return st;
         if (needed) *needed = total;
         if (total > cap) {
-            if (d2h_staged(ix, out_loc_offsets, d + o_loff, (n + 1) * 8, s) != hipSuccess) return FMX_E_DEVICE;
+            if (ix->stage.d2h(out_loc_offsets, d + o_loff, (n + 1) * 8, s) != hipSuccess) return FMX_E_DEVICE;
             return FMX_E_CAPACITY;
         }
         if (total <= dcap) {
-            e = d2h_staged(ix, out_loc_offsets, d + o_loff, (n + 1) * 8, s);
-            if (e == hipSuccess && total) e = d2h_staged(ix, out_locs, d + o_locs, total * pb, s);
+            e = ix->stage.d2h(out_loc_offsets, d + o_loff, (n + 1) * 8, s);
+            if (e == hipSuccess && total) e = ix->stage.d2h(out_locs, d + o_locs, total * pb, s);
             return dev_err(e);
         }
         dcap = total;  // second pass with room for every location
@@ -1328,10 +1428,16 @@ fmx_status fmx_build(const uint8_t *text, uint64_t text_len, const uint8_t *tabl
     if (hipMalloc(&dt, std::max<uint64_t>(text_len, 1)) != hipSuccess) return FMX_E_DEVICE;
     if (hipMalloc(&db, std::max<uint64_t>(blob_len, 16)) != hipSuccess) { hipFree(dt); return FMX_E_DEVICE; }
     fmx_status st = FMX_OK;
-    if (text_len && hipMemcpy(dt, text, text_len, hipMemcpyHostToDevice) != hipSuccess) st = FMX_E_DEVICE;
-    if (!st) st = fmx_build_device(dt, text_len, table, symbol_count, layout, kmer_size, sampling_ratio, db,
-                                   blob_len, device);
-    if (!st && hipMemcpy(blob, db, blob_len, hipMemcpyDeviceToHost) != hipSuccess) st = FMX_E_DEVICE;
+    {
+        // the caller's text and blob through a pinned stage (no DMA on their
+        // pageable pages); fmx_build_device starts after the text's copies
+        // (hipDeviceSynchronize) and has finished when it returns
+        Stage io(32ull << 20);
+        if (text_len && io.h2d(dt, text, text_len, nullptr) != hipSuccess) st = FMX_E_DEVICE;
+        if (!st) st = fmx_build_device(dt, text_len, table, symbol_count, layout, kmer_size, sampling_ratio, db,
+                                       blob_len, device);
+        if (!st && io.d2h(blob, db, blob_len, nullptr) != hipSuccess) st = FMX_E_DEVICE;
+    }
     hipFree(dt);
     hipFree(db);
     return st;

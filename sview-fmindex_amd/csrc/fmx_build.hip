@@ -354,22 +354,21 @@ static hipError_t max_scan(const uint32_t *in, uint32_t *out, size_t m, hipStrea
 }
 
 static hipError_t select_active(const uint32_t *in, const uint8_t *flags, uint32_t *out, size_t m, uint64_t *d_count,
-                                uint64_t *h_count, hipStream_t s) {
+                                uint64_t *h_count, Stage &io, hipStream_t s) {
     size_t tb = 0;
     hipError_t e = rocprim::select(nullptr, tb, in, flags, out, d_count, m, s);
     if (e != hipSuccess) return e;
     e = with_temp(tb, [&](void *tmp) { return rocprim::select(tmp, tb, in, flags, out, d_count, m, s); });
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return e;
-    return hipStreamSynchronize(s);
+    return io.d2h(h_count, d_count, 8, s);  // (synchronous)
 }
 
 // Suffix array of t[0..n1) (t[n1-1] == 0 unique) into sa (u32), by prefix
 // doubling: sort by the packed first K0 symbols, then repeatedly re-sort only
 // the unresolved groups by (rank[i], rank[i+h]), h = K0, 2K0, 4K0, ...
 // Ranks are group-head slots, so every key fits 32 + 32 bits.
-static fmx_status suffix_array(const uint8_t *t, uint64_t n1, uint32_t alphabet, uint32_t *sa, hipStream_t s) {
+static fmx_status suffix_array(const uint8_t *t, uint64_t n1, uint32_t alphabet, uint32_t *sa, Stage &io,
+                               hipStream_t s) {
     uint32_t b = 1;
     while ((1u << b) < alphabet) ++b;
     const uint32_t K0 = 64 / b;
@@ -394,7 +393,7 @@ static fmx_status suffix_array(const uint8_t *t, uint64_t n1, uint32_t alphabet,
     }
     uint64_t m = 0;
     uint32_t *A = act.as<uint32_t>(), *A2 = act2.as<uint32_t>();
-    BCK(select_active(HV, FL, A, n1, cntd.as<uint64_t>(), &m, s));
+    BCK(select_active(HV, FL, A, n1, cntd.as<uint64_t>(), &m, io, s));
     for (uint64_t h = K0; m > 0; h *= 2) {
         if (h >= n1) return FMX_E_CONFIG;  // impossible with a unique sentinel
         uint64_t *k1 = kA.as<uint64_t>(), *k2 = kB.as<uint64_t>();
@@ -407,7 +406,7 @@ static fmx_status suffix_array(const uint8_t *t, uint64_t n1, uint32_t alphabet,
         hipLaunchKernelGGL(k_round_write, dim3(grid_of(m)), dim3(256), 0, s, A, m, v1, HJ, sa, ISA);
         BCK(hipGetLastError());
         uint64_t m2 = 0;
-        BCK(select_active(A, FL, A2, m, cntd.as<uint64_t>(), &m2, s));
+        BCK(select_active(A, FL, A2, m, cntd.as<uint64_t>(), &m2, io, s));
         std::swap(A, A2);
         m = m2;
     }
@@ -562,7 +561,7 @@ static hipError_t max_scan64(const uint64_t *in, uint64_t *out, size_t m, hipStr
 
 // slots j in [s0, s0 + m) with flags[j] set, appended to out[*count...]
 static hipError_t select_slots(const uint8_t *flags, uint64_t s0, uint64_t m, uint64_t *out, uint64_t *d_count,
-                               uint64_t *h_count, hipStream_t s) {
+                               uint64_t *h_count, Stage &io, hipStream_t s) {
     DBuf idx;
     hipError_t e = idx.alloc(m * 8);
     if (e != hipSuccess) return e;
@@ -574,12 +573,11 @@ static hipError_t select_slots(const uint8_t *flags, uint64_t s0, uint64_t m, ui
         return rocprim::select(tmp, tb, idx.as<uint64_t>(), flags + s0, out, d_count, m, s);
     });
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(h_count, d_count, 8, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return e;
-    return hipStreamSynchronize(s);
+    return io.d2h(h_count, d_count, 8, s);  // (synchronous)
 }
 
-static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabet, uint64_t *sa, hipStream_t s) {
+static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabet, uint64_t *sa, Stage &io,
+                                 hipStream_t s) {
     uint32_t b = 1;
     while ((1u << b) < alphabet) ++b;
     const uint32_t K0 = 64 / b, W = alphabet, B2 = W * W;
@@ -598,8 +596,7 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
         hipLaunchKernelGGL(k_bucket_of, dim3(G), dim3(256), B2 * 4, s, t, n1, W, hist.as<uint32_t>());
         BCK(hipGetLastError());
         std::vector<uint32_t> hh((size_t)G * B2);
-        BCK(hipMemcpyAsync(hh.data(), hist.p, hh.size() * 4, hipMemcpyDeviceToHost, s));
-        BCK(hipStreamSynchronize(s));
+        BCK(io.d2h(hh.data(), hist.p, hh.size() * 4, s));
         std::vector<uint64_t> hb((size_t)G * B2);
         uint64_t run = 0;
         for (uint32_t bk = 0; bk < B2; ++bk) {
@@ -610,7 +607,7 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
             }
         }
         bstart[B2] = run;
-        BCK(hipMemcpyAsync(base.p, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, s));
+        BCK(io.h2d(base.p, hb.data(), hb.size() * 8, s));
         hipLaunchKernelGGL(k_bucket_scatter, dim3(G), dim3(256), B2 * 8, s, t, n1, W, base.as<uint64_t>(), sa);
         BCK(hipGetLastError());
         BCK(hipStreamSynchronize(s));
@@ -651,7 +648,7 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
         for (uint32_t bk = 0; bk < B2; ++bk) {
             const uint64_t s0 = bstart[bk], mm = bstart[bk + 1] - s0;
             if (!mm) continue;
-            BCK(select_slots(ACT, s0, mm, tmpl.as<uint64_t>(), cntd.as<uint64_t>(), &part[bk], s));
+            BCK(select_slots(ACT, s0, mm, tmpl.as<uint64_t>(), cntd.as<uint64_t>(), &part[bk], io, s));
             total += part[bk];
         }
         BCK(alist.alloc(std::max<uint64_t>(total, 1) * 8));
@@ -659,7 +656,7 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
             const uint64_t s0 = bstart[bk], mm = bstart[bk + 1] - s0;
             if (!part[bk]) continue;
             uint64_t got = 0;
-            BCK(select_slots(ACT, s0, mm, alist.as<uint64_t>() + m, cntd.as<uint64_t>(), &got, s));
+            BCK(select_slots(ACT, s0, mm, alist.as<uint64_t>() + m, cntd.as<uint64_t>(), &got, io, s));
             m += got;
         }
     }
@@ -700,8 +697,7 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
             BCK(with_temp(tb, [&](void *tmp) {
                 return rocprim::select(tmp, tb, A, fl, A2, cntd.as<uint64_t>(), m, s);
             }));
-            BCK(hipMemcpyAsync(&m2, cntd.p, 8, hipMemcpyDeviceToHost, s));
-            BCK(hipStreamSynchronize(s));
+            BCK(io.d2h(&m2, cntd.p, 8, s));
         }
         BCK(hipMemcpyAsync(A, A2, m2 * 8, hipMemcpyDeviceToDevice, s));
         m = m2;
@@ -712,7 +708,8 @@ static fmx_status suffix_array64(const uint8_t *t, uint64_t n1, uint32_t alphabe
 
 template <typename P>
 static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *table, uint32_t sigma, fmx_layout L,
-                              uint32_t k, uint32_t sr, uint8_t *d_blob, const BlobSizes &S, hipStream_t s) {
+                              uint32_t k, uint32_t sr, uint8_t *d_blob, const BlobSizes &S, Stage &io,
+                              hipStream_t s) {
     const uint64_t W = sigma + 1, n1 = n + 1;
     // ---- headers (builder/mod.rs:211-231) -------------------------------
     std::vector<uint8_t> hdr(S.header, 0);
@@ -730,7 +727,7 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
     h += S.sah;
     w32(h, sigma); w64(h + 8, S.ckpt_len); w64(h + 16, S.blocks_len);
     BCK(hipMemsetAsync(d_blob, 0, S.total, s));
-    BCK(hipMemcpyAsync(d_blob, hdr.data(), S.header, hipMemcpyHostToDevice, s));
+    BCK(io.h2d(d_blob, hdr.data(), S.header, s));
     uint8_t *body = d_blob + S.header;
     uint8_t *ca = body, *mult = ca + S.ca, *kt = mult + S.mult, *sa_out = kt + S.kt;
     uint8_t *sent = sa_out + S.sa, *ckpt = sent + S.sent, *blocks = ckpt + S.ckpt;
@@ -746,9 +743,8 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
     BCK(hipGetLastError());
     uint32_t hstatus = 0;
     uint64_t hsym[kMaxSigma];
-    BCK(hipMemcpyAsync(&hstatus, st.p, 4, hipMemcpyDeviceToHost, s));
-    BCK(hipMemcpyAsync(hsym, symc.p, kMaxSigma * 8, hipMemcpyDeviceToHost, s));
-    BCK(hipStreamSynchronize(s));
+    BCK(io.d2h(&hstatus, st.p, 4, s));
+    BCK(io.d2h(hsym, symc.p, kMaxSigma * 8, s));
     if (hstatus) return FMX_E_SYMBOL;  // idx >= symbol_count: the reference panics
     std::vector<uint8_t> cah(W * sizeof(P)), mh(k * 8);
     uint64_t acc = 0;
@@ -762,8 +758,8 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
         for (uint32_t j = 0; j < k - 1 - i; ++j) p *= W;
         memcpy(&mh[i * 8], &p, 8);
     }
-    BCK(hipMemcpyAsync(ca, cah.data(), cah.size(), hipMemcpyHostToDevice, s));
-    BCK(hipMemcpyAsync(mult, mh.data(), mh.size(), hipMemcpyHostToDevice, s));
+    BCK(io.h2d(ca, cah.data(), cah.size(), s));
+    BCK(io.h2d(mult, mh.data(), mh.size(), s));
     BCK(kh.alloc(S.kt_len * 8)); BCK(khs.alloc(S.kt_len * 8));
     BCK(hipMemsetAsync(kh.p, 0, S.kt_len * 8, s));
     const size_t lds = S.kt_len <= 8192 ? S.kt_len * 4 : 0;
@@ -789,8 +785,8 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
     const bool sa64 = n1 >= 0xFFFFFFFFull || (force64 && atoi(force64) != 0);
     DBuf sab;
     BCK(sab.alloc(n1 * (sa64 ? 8 : 4)));
-    fmx_status fs = sa64 ? suffix_array64(t, n1, (uint32_t)W, sab.as<uint64_t>(), s)
-                         : suffix_array(t, n1, (uint32_t)W, sab.as<uint32_t>(), s);
+    fmx_status fs = sa64 ? suffix_array64(t, n1, (uint32_t)W, sab.as<uint64_t>(), io, s)
+                         : suffix_array(t, n1, (uint32_t)W, sab.as<uint32_t>(), io, s);
     if (fs) return fs;
 
     // ---- 3. pidx, stored BWT, sampled SA ----------------------------------
@@ -844,8 +840,7 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
                        tot.as<uint64_t>());
     BCK(hipGetLastError());
     std::vector<uint64_t> htot(chunks * sigma);
-    BCK(hipMemcpyAsync(htot.data(), tot.p, htot.size() * 8, hipMemcpyDeviceToHost, s));
-    BCK(hipStreamSynchronize(s));
+    BCK(io.d2h(htot.data(), tot.p, htot.size() * 8, s));
     {
         std::vector<uint64_t> run(sigma, 0);
         for (uint64_t g = 0; g < chunks; ++g)
@@ -855,7 +850,7 @@ static fmx_status build_typed(const uint8_t *d_text, uint64_t n, const uint8_t *
                 run[c] += v;
             }
     }
-    BCK(hipMemcpyAsync(tot.p, htot.data(), htot.size() * 8, hipMemcpyHostToDevice, s));
+    BCK(io.h2d(tot.p, htot.data(), htot.size() * 8, s));
     hipLaunchKernelGGL(k_ckpt<P>, dim3((unsigned)chunks), dim3(256), 0, s, cnt.as<uint8_t>(), S.blocks_len, sigma,
                        tot.as<uint64_t>(), (P *)ckpt);
     BCK(hipGetLastError());
@@ -871,8 +866,12 @@ fmx_status build_device(const uint8_t *d_text, uint64_t n, const uint8_t *table,
     if (st) return st;
     if (blob_len != S.total) return FMX_E_CONFIG;                      // BuildError::InvalidBlobSize
     if (((uintptr_t)d_blob) % (L.vec_bits == 128 ? 16 : 8)) return FMX_E_ALIGN;  // NotAlignedBlob
-    if (L.pos_bytes == 4) return build_typed<uint32_t>(d_text, n, table, sigma, L, k, sr, d_blob, S, s);
-    return build_typed<uint64_t>(d_text, n, table, sigma, L, k, sr, d_blob, S, s);
+    // every host <-> device copy of the build (headers, counts, totals)
+    // through a pinned stage; its destructor waits for the copies still in
+    // flight, on every return path
+    Stage io(1ull << 20);
+    if (L.pos_bytes == 4) return build_typed<uint32_t>(d_text, n, table, sigma, L, k, sr, d_blob, S, io, s);
+    return build_typed<uint64_t>(d_text, n, table, sigma, L, k, sr, d_blob, S, io, s);
 }
 
 }  // namespace fmx

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <deque>
 #include <functional>
@@ -122,6 +123,40 @@ struct Timer {
     uint64_t units = 0;
 };
 
+// Pinned staging for every copy between host memory the engine does not own
+// (the caller's buffers, its own locals and vectors) and HBM: the CPU copies
+// between those pages and two pinned buffers, the DMA engine only ever reads
+// or writes the pinned buffers.  No DMA touches pageable memory, so no copy
+// depends on how the runtime pins or stages it, and none can outlive the
+// host buffer it came from (round 4).  Double-buffered: the
+// CPU copy of one chunk overlaps the DMA of the previous one, and a buffer
+// is refilled only after the event recorded behind its last copy.
+//   h2d: returns once the source has been copied into the stage; the DMA is
+//        ordered on `s` (later work on `s` sees the bytes).
+//   d2h: synchronous — returns once the bytes are in the caller's buffer.
+// One mutex per stage: calls from several threads take turns.
+struct Stage {
+    explicit Stage(uint64_t max_chunk = 8ull << 20) : max_chunk_(max_chunk) {}
+    Stage(const Stage &) = delete;
+    Stage &operator=(const Stage &) = delete;
+    ~Stage();
+    hipError_t h2d(void *d, const void *h, uint64_t n, hipStream_t s);
+    hipError_t d2h(void *h, const void *d, uint64_t n, hipStream_t s);
+    hipError_t drain();  // every copy from or into the stage has completed
+    uint64_t chunk_bytes() const { return chunk_; }
+
+  private:
+    hipError_t reserve(uint64_t n);
+    hipError_t wait(int b);
+    uint8_t *buf_[2] = {nullptr, nullptr};
+    hipEvent_t ev_[2] = {nullptr, nullptr};
+    bool pending_[2] = {false, false};
+    int next_ = 0;
+    uint64_t chunk_ = 0;
+    const uint64_t max_chunk_;
+    std::mutex mu_;
+};
+
 // A status word's owner: the stream it is assigned to, its recency (for
 // least-recently-used recycling) and what is known about its launches: a
 // slot is recycled only when its stream is known to be idle.  Completion
@@ -164,6 +199,9 @@ struct fmx_index {
     // groups every launch that can be, FMX_GROUPED=0 none; the key = the last
     // gkey_len symbols, digits over the gkey_base symbols that occur in the text
     uint64_t grouped_min = 0;
+    // launches of this index by path (fmx_index_info): grouped (packed / id-only records) and in
+    // launch order — the tests assert which path a launch took
+    mutable std::atomic<uint64_t> launches_grouped{0}, launches_grouped_raw{0}, launches_ordered{0};
     uint32_t gkey_len = 0, gkey_base = 0;
     uint32_t grouped_xcd = 0;  // each XCD searches one eighth of the key order (default; FMX_GROUPED_XCD=0 off)
     uint32_t grouped_pair = 0; // FMX_GROUPED_PAIR=1: two patterns per lane in the grouped search
@@ -190,10 +228,9 @@ struct fmx_index {
     // host-API scratch (grown on demand) and its private locate workspace
     uint8_t *d_scratch = nullptr;
     uint64_t scratch_bytes = 0;
-    // pinned host staging of the host-API calls (fmx_count_batch / fmx_locate_batch): the caller's
-    // pageable buffers are only ever memcpy'd by the CPU; the DMA engine reads and writes this
-    uint8_t *h_stage = nullptr;
-    uint64_t h_stage_bytes = 0;
+    // pinned host staging of every host-memory copy of the index (the host-API batches, status
+    // words, totals): the caller's pageable buffers are only ever memcpy'd by the CPU
+    fmx::Stage stage;
     uint8_t *d_ws = nullptr;
     uint64_t ws_bytes = 0;
     // timing

@@ -102,9 +102,15 @@ fmx_status fmx_multi_load(const uint8_t *blob, uint64_t blob_len, fmx_layout lay
             free_multi(m);
             return FMX_E_DEVICE;
         }
-    // host -> the first device once; the first device -> every other replica
+    // host -> the first device once (through a pinned stage: no DMA on the
+    // caller's pageable blob); the first device -> every other replica
     hipError_t e = hipSetDevice(devices[0]);
-    if (e == hipSuccess && blob_len) e = hipMemcpy(m->d_blobs[0], blob, blob_len, hipMemcpyHostToDevice);
+    if (e == hipSuccess && blob_len) {
+        Stage up(32ull << 20);
+        e = up.h2d(m->d_blobs[0], blob, blob_len, nullptr);
+        if (e == hipSuccess) e = up.drain();
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
     for (int d = 1; d < n_devices && e == hipSuccess; ++d)
         if (blob_len) e = hipMemcpyPeer(m->d_blobs[d], devices[d], m->d_blobs[0], devices[0], blob_len);
     if (e != hipSuccess) {

@@ -456,6 +456,8 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const L
     hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, stream)
                            : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
+    (grouped ? (raw ? ix->launches_grouped_raw : ix->launches_grouped) : ix->launches_ordered)
+        .fetch_add(1, std::memory_order_relaxed);
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     uint32_t fold = 1;
     for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;

@@ -93,7 +93,10 @@ class JobGather:
     kernels write batch j's counts and locations into (locations capacity =
     needs[rank][j] exactly)."""
 
-    def __init__(self, sizes, needs, group: int, rank: int, dtype, device, pg=None):
+    def __init__(self, sizes, needs, group: int, rank: int, dtype, device, pg=None, collective=None):
+        """collective: gather over the process group even with one rank (a
+        one-GPU run that drives the RCCL path: bench.py with FMX_BENCH_DIST=1);
+        default: only with several ranks."""
         import torch
         self.sizes = np.asarray(sizes, dtype=np.int64)
         self.needs = np.asarray(needs, dtype=np.int64)
@@ -111,9 +114,10 @@ class JobGather:
             self.loc[:, g] = self.needs[:, sl].sum(axis=1)
         self.slab = [max(1, int((self.cnt[:, g] + self.loc[:, g]).max())) for g in range(self.ngroups)]
         self.inp = [torch.zeros(s, dtype=dtype, device=device) for s in self.slab]
-        # one rank: the slab is its own result (nothing to gather)
-        self.out = self.inp if self.world == 1 else [torch.zeros(self.world * s, dtype=dtype, device=device)
-                                                      for s in self.slab]
+        self.collective = self.world > 1 if collective is None else bool(collective)
+        # no collective (one rank): the slab is its own result
+        self.out = [torch.zeros(self.world * s, dtype=dtype, device=device)
+                    for s in self.slab] if self.collective else self.inp
 
     def _where(self, j: int):
         g = j // self.group
@@ -132,7 +136,7 @@ class JobGather:
     def gather(self, g: int, async_op: bool = False):
         """Group g's all-gather (enqueue it on a communication stream to
         overlap it with the next launch); None with one rank."""
-        if self.world == 1:
+        if not self.collective:
             return None
         return _all_gather_flat(self.out[g], self.inp[g], self.pg, async_op)
 
@@ -265,6 +269,40 @@ class ShardedLocate:
         self.last = {"patterns": n, "shard": (s, e), "bytes_gathered": self.world * S * inp.element_size(),
                      "result_bytes": int((parts[:, 0] + parts[:, 1]).sum()) * inp.element_size()}
         return offsets, torch.cat(locs)
+
+
+def workspace_bytes(n: int, pos_bytes: int) -> int:
+    """fmx_locate_workspace_size for n patterns (fmx_api.cpp ws_bytes_for):
+    [256 B + 4 x 4,096 key counters][tile counts and offsets: 2 x 8 B per
+    256-pattern tile][search records: 16 B (u32) / 24 B (u64) per
+    pattern][16 B][sorted order: 16 B per pattern]."""
+    tiles = max(1, -(-int(n) // 256))
+    return 256 + 4 * 4096 + 16 * tiles + int(n) * (16 if pos_bytes == 4 else 24) + 16 + 16 * int(n)
+
+
+def hbm_per_rank(*, blob: int, records: int, text: int, batch_sizes: Sequence[int], m: int, pos_bytes: int,
+                 world: int, group: int, loc_cap: Sequence[int], gather: bool) -> dict:
+    """HBM one rank of bench.py holds (bytes), by part: the replicated blob and
+    its interleaved occ records; the synthetic text the patterns are cut from;
+    per batch its patterns (m B each), offsets and output offsets (8 B per
+    pattern + 8), counts (P), locations (loc_cap[j] x P) and workspace; with
+    gathers (several ranks, or the RCCL path at one rank) the JobGather slabs —
+    per launch group this rank's part (its counts + locations) and the
+    gathered output, world x the largest rank's part (taken as this rank's:
+    random patterns make the parts near-equal)."""
+    P = int(pos_bytes)
+    sizes = [int(b) for b in batch_sizes]
+    caps = [int(c) for c in loc_cap]
+    batches = sum(b * m + 2 * 8 * (b + 1) + 8 + b * P + c * P + workspace_bytes(b, P) for b, c in zip(sizes, caps))
+    slabs = 0
+    if gather:
+        for g in range(0, len(sizes), group):
+            part = (sum(sizes[g:g + group]) + sum(caps[g:g + group])) * P
+            slabs += part + world * part
+    parts = {"blob": int(blob), "occ_records": int(records), "text": int(text), "batches": batches,
+             "gather_slabs": slabs}
+    parts["total"] = sum(parts.values())
+    return parts
 
 
 def all_gather_ints(values: Sequence[int], device=None, pg=None) -> np.ndarray:

@@ -128,12 +128,18 @@ hipError_t run_grid(dim3 grid, dim3 block, size_t dyn_lds_bytes, const std::func
 void set_last_error(hipError_t e);
 void land_before_launch(hipStream_t s);
 
+// Runs `launch` now, or (deferred streams, simt_defer) queues it on s:
+// then a failure is reported by the next synchronisation of s, as on the GPU.
+hipError_t submit_launch(hipStream_t s, std::function<hipError_t()> launch);
+
 template <class... KP, class... A>
 hipError_t launch_kernel(void (*k)(KP...), dim3 g, dim3 b, size_t lds, hipStream_t s, A &&...a) {
     static_assert(sizeof...(KP) == sizeof...(A), "kernel argument count");
-    land_before_launch(s);
     auto args = std::make_shared<std::tuple<std::decay_t<KP>...>>(std::forward<A>(a)...);
-    const hipError_t e = run_grid(g, b, lds, [k, args]() { std::apply(k, *args); });
+    const hipError_t e = submit_launch(s, [k, args, g, b, lds, s]() {
+        land_before_launch(s);
+        return run_grid(g, b, lds, [k, args]() { std::apply(k, *args); });
+    });
     if (e != hipSuccess) set_last_error(e);
     return e;
 }

@@ -24,6 +24,16 @@
 // non-blocking stream is not ordered after the null stream).  A kernel on
 // such a stream that reads the destination without a synchronisation reads
 // whatever was there before.
+// Deferred streams (simt_defer(), SIMT_DEFER=1): work on a non-null stream —
+// kernels, copies, memsets, event records, waits on events — is queued and
+// runs in stream order at a random later time (at random points of later
+// host API calls), and at the latest when the host synchronises with it
+// (hipStreamSynchronize, hipEventSynchronize, a completed hipEventQuery,
+// hipDeviceSynchronize, hipFree).  A copy reads its source and writes its
+// destination when it runs, as a DMA engine does: a host buffer reused before
+// the copy that reads it has run, or read before the copy that fills it has
+// run, gives wrong bytes.  A deferred kernel's failure is reported by the
+// next synchronisation of its stream.
 // SIMT_SEED sets the random stream (simt_config() from a test).
 #include <hip/hip_runtime.h>
 
@@ -34,11 +44,14 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <deque>
 #include <cstdlib>
 #include <mutex>
 #include <random>
 #include <string>
 #include <vector>
+
+extern "C" void simt_defer(int on, double progress);
 
 extern "C" {
 extern char __start_simt_lds[] __attribute__((weak, visibility("hidden")));
@@ -165,6 +178,7 @@ void init_once() {
     sigaction(SIGBUS, &sa, nullptr);
     if (const char *s = getenv("SIMT_SEED")) g_rng.seed(strtoull(s, nullptr, 0));
     if (const char *y = getenv("SIMT_YIELD")) g_yield = atof(y);
+    if (const char *d = getenv("SIMT_DEFER")) simt_defer(atoi(d), 0.25);
 }
 
 uint64_t rnd() { return g_rng(); }
@@ -423,6 +437,134 @@ void land_pending() {
 bool null_stream(hipStream_t s) { return s == nullptr; }
 }  // namespace
 
+// ------------------------------------------------------- deferred streams
+struct simt_stream {
+    std::deque<std::function<void()>> q;  // queued, not run yet (deferred mode)
+    uint64_t issued = 0, done = 0;        // operations queued / run so far
+    hipError_t err = hipSuccess;          // a deferred kernel's failure, until the next sync
+};
+struct simt_event {
+    simt_stream *s = nullptr;  // null: complete
+    uint64_t seq = 0;          // complete once s->done >= seq
+};
+
+namespace {
+std::recursive_mutex g_q_mu;
+bool g_defer = false;
+double g_progress = 0.25;  // chance that a host API call runs some queued work
+std::mt19937_64 g_q_rng(0xdefe);
+std::vector<simt_stream *> g_streams;  // (never freed: events may outlive their stream)
+int g_q_depth = 0;
+
+void drain(simt_stream *s, uint64_t upto) {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    ++g_q_depth;
+    while (s->done < upto && !s->q.empty()) {
+        std::function<void()> f = std::move(s->q.front());
+        s->q.pop_front();
+        ++s->done;
+        f();
+    }
+    --g_q_depth;
+}
+
+void drain_all() {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    for (size_t i = 0; i < g_streams.size(); ++i) drain(g_streams[i], g_streams[i]->issued);
+}
+
+// at random points of host API calls: a random stream runs a random prefix of its queue
+void maybe_progress() {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    if (!g_defer || g_q_depth || g_streams.empty()) return;
+    if (std::uniform_real_distribution<double>(0.0, 1.0)(g_q_rng) >= g_progress) return;
+    simt_stream *s = g_streams[g_q_rng() % g_streams.size()];
+    if (s->q.empty()) return;
+    drain(s, s->done + 1 + g_q_rng() % s->q.size());
+}
+
+// run f now (immediate mode, the null stream) or queue it on s
+void submit(hipStream_t s, std::function<void()> f) {
+    std::unique_lock<std::recursive_mutex> g(g_q_mu);
+    if (!g_defer || null_stream(s)) {
+        if (s) { ++s->issued; ++s->done; }
+        g.unlock();
+        f();
+        return;
+    }
+    s->q.push_back(std::move(f));
+    ++s->issued;
+    maybe_progress();
+}
+}  // namespace
+
+namespace simt {
+hipError_t submit_launch(hipStream_t s, std::function<hipError_t()> launch) {
+    {
+        std::lock_guard<std::recursive_mutex> g(g_q_mu);
+        if (!g_defer || null_stream(s)) {
+            if (s) { ++s->issued; ++s->done; }
+        } else {
+            s->q.push_back([s, launch]() {
+                const hipError_t e = launch();
+                if (e != hipSuccess && s->err == hipSuccess) s->err = e;
+            });
+            ++s->issued;
+            maybe_progress();
+            return hipSuccess;
+        }
+    }
+    return launch();
+}
+}  // namespace simt
+
+extern "C" {
+// TEST hook: deferred streams on / off (from now on; queued work is run first)
+// and the chance that a host API call runs some queued work.
+void simt_defer(int on, double progress) {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    drain_all();
+    g_defer = on != 0;
+    g_progress = progress;
+}
+// TEST hook: the deferred-stream model itself (0 = as specified): a queued
+// host-to-device copy reads its source when it runs, a queued device-to-host
+// copy has not written its destination before the host synchronises, an
+// event orders both.
+int simt_selftest_defer() {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    const bool was = g_defer;
+    const double p = g_progress;
+    g_defer = true;
+    g_progress = 0.0;
+    int bad = 0;
+    hipStream_t s;
+    hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    void *dv = nullptr;
+    hipMallocRaw(&dv, 64);
+    uint8_t *d = static_cast<uint8_t *>(dv), h[64], o[64];
+    std::memset(h, 1, 64);
+    hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, s);
+    std::memset(h, 2, 64);  // reused before the copy has run
+    hipStreamSynchronize(s);
+    bad |= d[0] != 2 ? 1 : 0;
+    std::memset(o, 0, 64);
+    hipMemcpyAsync(o, d, 64, hipMemcpyDeviceToHost, s);
+    bad |= o[63] != 0 ? 2 : 0;  // not written before the host waits for it
+    hipEvent_t e;
+    hipEventCreate(&e);
+    hipEventRecord(e, s);
+    bad |= s->done == s->issued ? 4 : 0;
+    hipEventSynchronize(e);
+    bad |= o[63] != 2 ? 8 : 0;
+    hipEventDestroy(e);
+    g_defer = was;
+    g_progress = p;
+    free(dv);
+    return bad;
+}
+}
+
 namespace simt {
 // before a launch: on the null stream every staged copy lands first; on
 // another stream each lands with probability 1/2
@@ -468,7 +610,8 @@ hipError_t hipMallocRaw(void **p, size_t n) {
     return hipSuccess;
 }
 hipError_t hipFree(void *p) {
-    land_pending();  // (hipFree synchronises the device)
+    drain_all();     // (hipFree synchronises the device)
+    land_pending();
     free(p);
     return hipSuccess;
 }
@@ -487,7 +630,9 @@ hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind k) {
 }
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st) {
     if (null_stream(st)) return hipMemcpy(d, s, n, k);
-    if (n) std::memmove(d, s, n);
+    submit(st, [d, s, n]() {
+        if (n) std::memmove(d, s, n);
+    });
     return hipSuccess;
 }
 hipError_t hipMemcpyPeer(void *d, int, const void *s, int, size_t n) { return hipMemcpy(d, s, n, hipMemcpyDefault); }
@@ -505,40 +650,81 @@ hipError_t hipMemset(void *d, int v, size_t n) {
 }
 hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t st) {
     if (null_stream(st)) return hipMemset(d, v, n);
-    memset_or_fault(d, v, n);
+    submit(st, [d, v, n]() { memset_or_fault(d, v, n); });
     return hipSuccess;
 }
 hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned) {
-    *s = reinterpret_cast<hipStream_t>(new Tag);
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    *s = new simt_stream;
+    g_streams.push_back(*s);
     return hipSuccess;
 }
 hipError_t hipStreamCreate(hipStream_t *s) { return hipStreamCreateWithFlags(s, 0); }
 hipError_t hipStreamDestroy(hipStream_t s) {
-    delete reinterpret_cast<Tag *>(s);
+    if (s) drain(s, s->issued);  // (its work completes; the record stays for events that name it)
     return hipSuccess;
 }
 hipError_t hipStreamSynchronize(hipStream_t s) {
-    if (null_stream(s)) land_pending();
+    if (null_stream(s)) {
+        land_pending();
+        return hipSuccess;
+    }
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    drain(s, s->issued);
+    const hipError_t e = s->err;
+    s->err = hipSuccess;
+    return e;
+}
+hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned) {
+    if (!e || !e->s) return hipSuccess;
+    simt_stream *es = e->s;
+    const uint64_t seq = e->seq;
+    if (null_stream(s)) {
+        drain(es, seq);
+        return hipSuccess;
+    }
+    submit(s, [es, seq]() { drain(es, seq); });  // (s runs on once es has reached the event)
     return hipSuccess;
 }
-hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 hipError_t hipEventCreate(hipEvent_t *e) {
-    *e = reinterpret_cast<hipEvent_t>(new Tag);
+    *e = new simt_event;
     return hipSuccess;
 }
 hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned) { return hipEventCreate(e); }
-hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
-hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
-hipError_t hipEventQuery(hipEvent_t) { return hipSuccess; }
-hipError_t hipEventElapsedTime(float *ms, hipEvent_t, hipEvent_t) {
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t s) {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    if (null_stream(s)) {
+        e->s = nullptr;
+        e->seq = 0;
+        return hipSuccess;
+    }
+    e->s = s;
+    e->seq = s->issued + 1;
+    submit(s, [] {});
+    return hipSuccess;
+}
+hipError_t hipEventSynchronize(hipEvent_t e) {
+    if (e && e->s) drain(e->s, e->seq);
+    return hipSuccess;
+}
+hipError_t hipEventQuery(hipEvent_t e) {
+    std::lock_guard<std::recursive_mutex> g(g_q_mu);
+    if (!e || !e->s || e->s->done >= e->seq) return hipSuccess;
+    if (g_q_rng() & 1) return hipErrorNotReady;
+    drain(e->s, e->seq);
+    return hipSuccess;
+}
+hipError_t hipEventElapsedTime(float *ms, hipEvent_t a, hipEvent_t b) {
+    if (hipEventQuery(a) != hipSuccess || hipEventQuery(b) != hipSuccess) return hipErrorNotReady;
     *ms = 0.001f;
     return hipSuccess;
 }
 hipError_t hipEventDestroy(hipEvent_t e) {
-    delete reinterpret_cast<Tag *>(e);
+    delete e;
     return hipSuccess;
 }
 hipError_t hipDeviceSynchronize() {
+    drain_all();
     land_pending();
     return hipSuccess;
 }

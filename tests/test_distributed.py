@@ -268,6 +268,91 @@ def test_job_gather_slots_one_rank(pkg):
     assert jg.bytes_per_pass() == jg.result_bytes()
 
 
+def _one_rank_collective_worker(rank, world, port, result_path):
+    """One rank with a process group (bench.py's FMX_BENCH_DIST=1 path): the
+    gathers are real collectives into a separate output, and assembly reads
+    the gathered copy."""
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as g
+    D = g.load_package().distributed
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    plan = D.JobPlan(10, 1, 3, 2)
+    needs = D.all_gather_ints([1, 2, 3, 0])
+    jg = D.JobGather(plan.sizes(), needs, 2, 0, torch.int32, "cpu", collective=True)
+    counts = [[1, 0, 0], [0, 1, 1], [1, 2], [0, 0]]
+    locs = [[7], [5, 9], [1, 2, 3], []]
+    for j in range(4):
+        jg.counts_slot(j).copy_(torch.tensor(counts[j], dtype=torch.int32))
+        jg.locs_slot(j).copy_(torch.tensor(locs[j], dtype=torch.int32))
+    separate = all(o.data_ptr() != i.data_ptr() for o, i in zip(jg.out, jg.inp))
+    before = jg.assemble()[1].tolist()  # (nothing gathered yet: zeros)
+    works = [jg.gather(gi, async_op=True) for gi in range(jg.ngroups)]
+    for wk in works:
+        wk.wait()
+    off, loc = jg.assemble()
+    flat = [c for cs in counts for c in cs]
+    ok = (separate and all(w is not None for w in works) and before == [0] * 6 and
+          off.tolist() == [0] + list(np.cumsum(flat)) and loc.tolist() == [7, 5, 9, 1, 2, 3])
+    with open(result_path, "w") as f:
+        json.dump({"ok": bool(ok)}, f)
+    dist.destroy_process_group()
+
+
+def test_one_rank_collective_gather_gloo(tmp_path):
+    """JobGather(collective=True) with one rank (bench.py under torchrun
+    --nproc-per-node 1 with FMX_BENCH_DIST=1, the RCCL rehearsal on a one-GPU
+    box): every group's results go through the collective into the gathered
+    slab, which assembly reads."""
+    import torch.multiprocessing as mp
+    out = tmp_path / "res.json"
+    mp.spawn(_one_rank_collective_worker, args=(1, _free_port(), str(out)), nprocs=1, join=True)
+    assert json.loads(out.read_text())["ok"]
+
+
+def _bench_configs():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("fmx_bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.CONFIGS
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_hbm_per_rank_world8(pkg, cfg):
+    """What one of 8 ranks holds in HBM under bench.py's shapes, by
+    distributed.hbm_per_rank (the accounting bench.py reports in its line):
+    c2 weak (512 batches of 100k per rank, gathers of 256 per launch group),
+    c3 / c5 strong (JobPlan's batches), with the blob (its exact size from
+    FmIndexBuilder.blob_size), interleaved records bounded by 128 B per block,
+    the text, every batch's buffers and workspace, the location room bench.py
+    starts with (b + b/8 + 4096) and the gather slabs — against one MI355X's
+    288 GB, with a wide margin."""
+    D = pkg.distributed
+    c = _bench_configs()[cfg]
+    world, B, m, P = 8, c["patterns"], c["m"], c["pos"]
+    GR = c.get("group", 8)
+    table = pkg.text_encoders.EncodingTable.from_symbols(c["symbols"])
+    block = getattr(pkg.blocks, f"Block{c['planes']}")(pkg.Vector(c["vec"]))
+    blob = pkg.FmIndexBuilder(c["text_len"], table.symbol_count(), table, pkg.u32 if P == 4 else pkg.u64, block) \
+        .set_lookup_table_config(pkg.build_config.LookupTableConfig.KmerSize(c["k"])) \
+        .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(c["sr"])).blob_size()
+    records = (c["text_len"] // c["vec"] + 1) * 128
+    if c["total"]:
+        plan = D.JobPlan(c["total"], world, B, GR)
+        sizes = [b - a for a, b in plan.batches(0)]
+    else:
+        sizes = [B] * 512  # bench.py's default c2: 512 distinct batches, two launch groups of 256
+    hbm = D.hbm_per_rank(blob=blob, records=records, text=c["text_len"], batch_sizes=sizes, m=m, pos_bytes=P,
+                         world=world, group=GR, loc_cap=[b + b // 8 + 4096 for b in sizes], gather=True)
+    assert hbm["total"] == sum(v for k, v in hbm.items() if k != "total")
+    assert hbm["total"] < 0.25 * 288e9, hbm  # (c2: ~12 GB, c5: ~21 GB)
+    if cfg == "c2":
+        # two launch groups of 25.6 M patterns: each rank's part ~230 MB with room, gathered x8
+        assert 3e9 < hbm["gather_slabs"] < 5e9, hbm
+
+
 @pytest.mark.parametrize("world,group,target", [(2, 2, 100), (3, 4, 60)])
 def test_gloo_job_gather_matches_single(tmp_path, world, group, target):
     """world 2 and 3 (ragged shards: 1001 patterns), several launch groups."""

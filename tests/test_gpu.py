@@ -85,23 +85,62 @@ def diagnose(pkg, ix, load, data, offsets, pats, goff, ooff):
     return "; ".join(out)
 
 
-def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True):
+class BufferWatch:
+    """Copies of the caller's buffers (patterns, offsets, blob) taken before
+    the oracle reads them, compared after the oracle call and after every GPU
+    call: a recurrence of the round-4 failure (the GPU answered
+    as if a few pattern bytes differed from the caller's buffer) classifies
+    itself — the message names the first call after which a buffer differed
+    from its copy, and where, or says that every buffer was intact."""
+
+    def __init__(self, **bufs):
+        self.bufs = bufs
+        self.copies = {k: np.array(v, copy=True) for k, v in bufs.items()}
+        self.first_change = None
+
+    def check(self, after):
+        if self.first_change:
+            return
+        for k, v in self.bufs.items():
+            if not np.array_equal(v, self.copies[k]):
+                at = np.flatnonzero(np.asarray(v).view(np.uint8) != self.copies[k].view(np.uint8))
+                self.first_change = f"{k} changed after {after} at bytes {at[:8].tolist()}"
+                return
+
+    def report(self):
+        return self.first_change or "caller's buffers intact after every call"
+
+
+def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True, expect_path=None):
+    """Counts and locations of `pats` on the GPU against the oracle, forward
+    (and reversed).  expect_path: "grouped" / "grouped_raw" / "ordered" —
+    the launch path the first locate must have taken (fmx_index_info's
+    launch counters)."""
     L = O.layout(pb, planes, vb, enc)
+    data, offsets = pkg.pack_patterns(pats)
+    watch = BufferWatch(data=data, offsets=offsets, blob=blob)
     orc = O.OracleIndex(blob, L)
     encoder = pkg.text_encoders.EncodingTable if enc == 0 else pkg.text_encoders.PassThrough
 
     def load():
         return pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), encoder, options=occ)
-    ix = load()
-    data, offsets = pkg.pack_patterns(pats)
     ooff, olocs = orc.locate_batch(data, offsets)
+    watch.check("the oracle")
+    ix = load()
+    watch.check("FmIndex.load")
     goff, glocs = ix.locate_batch((data, offsets))
+    watch.check("locate_batch")
+    if expect_path is not None:
+        info = ix.info()
+        took = {k: info["launches_" + k] for k in ("grouped", "grouped_raw", "ordered")}
+        assert took[expect_path] >= 1, f"the locate did not run {expect_path}: {took}"
     if not np.array_equal(goff, ooff):
         pytest.fail("per-pattern counts / offsets differ: " + diagnose(pkg, ix, load, data, offsets, pats, goff,
-                                                                        ooff))
-    assert np.array_equal(glocs, olocs), "locations differ (SA-row order)"
+                                                                        ooff) + "; " + watch.report())
+    assert np.array_equal(glocs, olocs), "locations differ (SA-row order); " + watch.report()
     cnt = ix.count_batch((data, offsets))
-    assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff))
+    watch.check("count_batch")
+    assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff)), "count path differs; " + watch.report()
     if reversed_too:
         rpats = [p[::-1] for p in pats]
         rc = ix.count_batch(rpats, reversed=True)
@@ -109,6 +148,8 @@ def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True
         roff, rlocs = ix.locate_batch(rpats, reversed=True)
         assert np.array_equal(roff, ooff) and np.array_equal(rlocs, olocs)
     ix.close()
+    watch.check("close")
+    assert watch.first_change is None, watch.report()
     return ooff, olocs
 
 

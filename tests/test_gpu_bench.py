@@ -13,12 +13,23 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run_bench(args, env_extra=None, timeout=900):
+def run_bench(args, env_extra=None, timeout=900, torchrun=0):
+    """bench.py as a child process; torchrun=N: under `python -m
+    torch.distributed.run --nproc-per-node N` (the driver's multi-GPU launch)."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "FMX_BENCH_BACKEND", "FMX_BENCH_DIST"):
         env.pop(k, None)
     env.update(env_extra or {})
-    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, capture_output=True,
+    launcher = [sys.executable, "-u"]
+    if torchrun:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        launcher += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun}",
+                     "--master-addr=127.0.0.1", f"--master-port={port}"]
+    p = subprocess.run(launcher + [os.path.join(ROOT, "bench.py")] + args, capture_output=True,
                        text=True, timeout=timeout, env=env)
     sys.stderr.write(p.stderr[-4000:])
     return p
@@ -48,6 +59,45 @@ def test_c3_full_job_one_gpu():
     assert g["plan"]["batches_per_rank"] % 128 == 0
     assert r["config"]["launch_order"].startswith("grouped")
     assert r["self_location_check"] and r["n_gpus"] == 1 and r["ranks"] == 1
+
+
+def test_rccl_world1_strong_job():
+    """The RCCL path on the one GPU of the box: bench.py
+    under torchrun --nproc-per-node 1 with the nccl backend and the process
+    group up for one rank (FMX_BENCH_DIST=1) — the blob self-broadcast and
+    checksum (replicate_blob), every launch group's results all-gathered by
+    RCCL inside the timed step (JobGather.gather), the job assembled from the
+    gathered slabs (assemble) and all 800,000 patterns checked against the
+    oracle (--verify-job).  So the driver's 8-GPU run is not this code's first
+    contact with RCCL."""
+    p = run_bench(["--config", "c3", "--text-len", "50000000", "--total-patterns", "800000", "--verify-job",
+                   "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
+                  env_extra={"FMX_BENCH_DIST": "1"}, torchrun=1)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = last_json(p.stdout)
+    assert r["backend"] == "nccl" and r["rccl_world_size"] == 1 and r["ranks"] == 1
+    g = r["gather"]
+    assert g["inside_timed_step"] and g["collectives_per_launch"] == 1 and g["assembly_ok"]
+    assert g["gathered_over_result"] <= 1.0 + 1e-9
+    rep = r["blob_replication"]
+    assert rep["identical"] and rep["bytes"] > 0 and "broadcast" in rep["how"]
+    assert r["parity"]["bit_exact_vs_cpu"] and r["parity"]["patterns"] == 800_000
+    assert r["hbm_per_rank"]["gather_slabs"] > 0
+
+
+def test_rccl_world1_weak_gather():
+    """c2-shaped weak scaling under torchrun with one RCCL rank: each launch
+    group's counts and locations all-gathered by RCCL inside the timed step;
+    the assembled results hold this rank's part intact."""
+    p = run_bench(["--config", "c2", "--text-len", "20000000", "--patterns", "20000", "--steps", "16",
+                   "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
+                  env_extra={"FMX_BENCH_DIST": "1"}, torchrun=1)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = last_json(p.stdout)
+    assert r["backend"] == "nccl" and r["rccl_world_size"] == 1 and r["scaling"] == "weak"
+    g = r["gather"]
+    assert g["inside_timed_step"] and g["collectives_per_launch"] == 1 and g["assembly_ok"]
+    assert g["assembled_patterns"] == r["config"]["distinct_batches"] * 20000
 
 
 def test_rccl_oversubscription_refused():

@@ -54,40 +54,52 @@ def run_config(pkg, O, n, alphabet, symbols, pos, planes, vec, m, npat, seed, ex
     del d_text, d_blob
     torch.cuda.empty_cache()
     offsets = np.arange(npat + 1, dtype=np.uint64) * m
-    # a few edge patterns: absent, wildcard-only, short (not so short that
-    # they occur millions of times: the oracle walks every row)
-    extra = [bytes(x) for x in extra]
-    if extra:
-        ex_d, ex_o = pkg.pack_patterns(extra)
-        pats = np.concatenate([pats, ex_d])
-        offsets = np.concatenate([offsets, ex_o[1:] + offsets[-1]])
+    # a few edge patterns (absent, wildcard-only, short — not so short that
+    # they occur millions of times: the oracle walks every row), answered in
+    # a call of their own: the fixed-length batch alone is what a grouped
+    # launch takes (a batch of mixed lengths always runs in launch order)
+    ex_d, ex_o = pkg.pack_patterns([bytes(x) for x in extra]) if extra else (None, None)
     orc = O.OracleIndex(blob, O.layout(pos, planes, vec, 0))
     ooff, olocs = orc.locate_batch(pats, offsets, threads=oracle_threads())
+    eoff, elocs = orc.locate_batch(ex_d, ex_o, threads=oracle_threads()) if extra else (None, None)
     cnts = np.diff(ooff)
     top = np.argsort(cnts)[-3:]
-    progress(f"oracle: {offsets.size - 1:,} patterns, {olocs.size:,} locations; most: "
+    progress(f"oracle: {npat:,} patterns, {olocs.size:,} locations; most: "
              + ", ".join(f"{bytes(pats[int(offsets[i]):int(offsets[i + 1])])!r} x{int(cnts[i])}" for i in top)
-             + f"; zero counts: {int((cnts[:npat] == 0).sum())}")
+             + f"; zero counts: {int((cnts == 0).sum())}")
     starts_h = starts.cpu().numpy()
-    runs = ((pkg._native.FMX_OPT_DEFAULT, None), (pkg._native.FMX_OPT_DEFAULT, "1"), (pkg._native.FMX_OCC_BLOB, None))
-    for options, grouped in runs:
-        saved = os.environ.get("FMX_GROUPED")
-        if grouped is not None:
-            os.environ["FMX_GROUPED"] = grouped  # (read at load)
+    # (load options, environment at load, the path the batch must take): the
+    # default index as loaded (100k patterns: below the grouping threshold,
+    # launch order), grouping forced on (packed records for C2 and C4, id-only
+    # records for C5's 150 bp), and the blob as laid out
+    raw = m * int(table.symbol_count()).bit_length() > 96
+    runs = ((pkg._native.FMX_OPT_DEFAULT, {}, "ordered"),
+            (pkg._native.FMX_OPT_DEFAULT, {"FMX_GROUPED": "1", "FMX_GROUPED_RAW": "1" if raw else "0"},
+             "grouped_raw" if raw else "grouped"),
+            (pkg._native.FMX_OCC_BLOB, {}, "ordered"))
+    for options, env, path in runs:
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)  # (read at load)
         try:
             ix = pkg.FmIndex.load(blob, position, block, table, options=options)
         finally:
-            if grouped is not None:
-                if saved is None:
-                    del os.environ["FMX_GROUPED"]
+            for k, v in saved.items():
+                if v is None:
+                    del os.environ[k]
                 else:
-                    os.environ["FMX_GROUPED"] = saved
+                    os.environ[k] = v
         goff, glocs = ix.locate_batch((pats, offsets))
-        assert np.array_equal(goff, ooff), f"offsets differ, options {options} grouped {grouped}"
-        assert np.array_equal(glocs, olocs), f"locations differ, options {options} grouped {grouped}"
+        info = ix.info()
+        took = {k: info["launches_" + k] for k in ("grouped", "grouped_raw", "ordered")}
+        assert took[path] == 1 and sum(took.values()) == 1, f"options {options} {env}: expected {path}, ran {took}"
+        assert np.array_equal(goff, ooff), f"offsets differ, options {options} {env}"
+        assert np.array_equal(glocs, olocs), f"locations differ, options {options} {env}"
         cnt = ix.count_batch((pats, offsets))
         assert np.array_equal(cnt.astype(np.uint64), np.diff(ooff))
-        progress(f"options {options} grouped {grouped}: bit-exact")
+        if extra:
+            xoff, xlocs = ix.locate_batch((ex_d, ex_o))
+            assert np.array_equal(xoff, eoff) and np.array_equal(xlocs, elocs), f"edge patterns, {options} {env}"
+        progress(f"options {options} {env}: {path}, bit-exact")
         ix.close()
     # the size-independent property: every cut pattern finds its own start
     own = np.zeros(npat, dtype=bool)

@@ -21,12 +21,20 @@ from _util import ALL_LAYOUTS, rand_chr_list, rand_pattern, rand_text, table_fro
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def grouped(monkeypatch):
+@pytest.fixture(params=["shipped", "refine_check"])
+def grouped(request, monkeypatch):
+    """Every grouped test twice: with the kernel sequence users get (grouping
+    forced on, otherwise the shipped defaults: refine off, check off,
+    in-workgroup sort on) and with the refine sort and the device check on."""
     monkeypatch.setenv("FMX_GROUPED", "1")
-    monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")  # k_group_refine on every grouped launch, however small
-    monkeypatch.setenv("FMX_GROUP_CHECK", "1")  # the device-side check of the sorted order (k_group_check_*)
+    for k in ("FMX_GROUP_REFINE_MIN", "FMX_GROUP_REFINE", "FMX_GROUP_CHECK", "FMX_GROUPED_WSORT",
+              "FMX_GROUPED_RAW", "FMX_GROUPED_MIN", "FMX_GROUPED_PAIR", "FMX_GROUPED_XCD"):
+        monkeypatch.delenv(k, raising=False)
+    if request.param == "refine_check":
+        monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")  # k_group_refine on every grouped launch, however small
+        monkeypatch.setenv("FMX_GROUP_CHECK", "1")  # the device-side check of the sorted order (k_group_check_*)
     monkeypatch.setenv("FMX_DEBUG", "1")  # (an FMX_E_DEVICE names its cause on stderr)
+    return request.param
 
 
 def pack_bits(sigma):
@@ -51,7 +59,7 @@ def test_every_layout_grouped(pkg, O, grouped, pb, planes, vb):
             pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=m)) for _ in range(40)]
             pats += [b"\x00" * m, chars[:1] * m, chars[-1:] * m]   # wildcard byte, single-symbol runs
             for occ in (0, 1):
-                T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+                T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, expect_path="grouped")
 
 
 @pytest.mark.parametrize("m", [1, 3, 20, 32])
@@ -210,15 +218,18 @@ def test_every_layout_grouped_raw(pkg, O, grouped, monkeypatch, pb, planes, vb):
             pats = [p for p in pats if len(p) == m]
             pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=m)) for _ in range(30)]
             for occ in (0, 1):
-                T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
+                T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ, expect_path="grouped_raw")
 
 
-@pytest.mark.parametrize("m,pb,planes,vb", [(150, 8, 3, 128), (150, 4, 3, 64), (97, 4, 3, 64), (33, 8, 4, 32)])
+@pytest.mark.parametrize("m,pb,planes,vb", [(150, 8, 3, 128), (150, 4, 3, 64), (97, 4, 3, 64), (33, 8, 4, 32),
+                                            (250, 8, 3, 128), (250, 4, 3, 64)])
 def test_long_patterns_grouped(pkg, O, grouped, m, pb, planes, vb):
     """C5's shape: patterns too long to pack into a 96-bit record (150 bp)
     are grouped with id-only records, on a 2 Mbp ACGT text with the ACGTN
     table; 20,000 cut patterns + absent, wildcard and single-symbol ones,
-    forward and reversed, every count and location against the oracle."""
+    forward and reversed, every count and location against the oracle.
+    m = 250 is longer than the search's LDS room for a raw pattern
+    (kGroupRawStage = 216): those lanes read their pattern bytes from HBM."""
     rng = np.random.default_rng(m * 13 + pb)
     table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
     text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=2_000_000).astype(np.uint8).tobytes()
@@ -226,4 +237,4 @@ def test_long_patterns_grouped(pkg, O, grouped, m, pb, planes, vb):
     pats = [text[s:s + m] for s in rng.integers(0, len(text) - m, size=20_000)]
     pats += [bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=m)) for _ in range(200)]
     pats += [b"N" * m, b"A" * m, b"\x00" * m]
-    T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1)
+    T.check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1, expect_path="grouped_raw")

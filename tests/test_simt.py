@@ -4,7 +4,8 @@ fmx_kernels.hpp, fmx_device.hpp — the C ABI, the launch logic and every
 kernel) compiled for the CPU against a SIMT shim (tests/simt): one fiber per
 work-item, workgroups in a shuffled order, work-items interleaved at random
 between barriers, atomics returning in a random order, LDS and device memory
-random until written.  The same Python API the GPU tests use runs on it, and
+random until written, stream work queued and run late (a copy reads and
+writes host memory when it runs).  The same Python API the GPU tests use runs on it, and
 every answer is compared with the oracle under many schedules (seeds), so a
 result that depends on scheduling, atomic order or unwritten memory fails here
 deterministically — on the CPU, with the failing seed in the message.
@@ -44,6 +45,14 @@ def simt(pkg):
     L.simt_stats.restype = None
     L.simt_memset_fault.argtypes = [C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64]
     L.simt_memset_fault.restype = None
+    L.simt_defer.argtypes = [C.c_int, C.c_double]
+    L.simt_defer.restype = None
+    L.simt_selftest_defer.argtypes = []
+    L.simt_selftest_defer.restype = C.c_int
+    # deferred streams for every test here: work queued on a stream runs at a
+    # random later host call or when the host synchronises, copies read and
+    # write host memory when they run (simt_rt.cpp)
+    L.simt_defer(1, 0.25)
     saved = n._lib
     n._lib = L
     yield L
@@ -342,3 +351,45 @@ def test_gpu_grouped_sweep_simt(pkg, O, simt, monkeypatch, pb, planes, vb):
         blob = O.build(text, sigma, O.layout(pb, planes, vb), k, sr, table)
         for occ in (0, 1):
             check_simt(pkg, O, blob, pb, planes, vb, pats, occ)
+
+
+def test_deferred_stream_model_simt(simt):
+    """The emulator's stream model (what the staging tests below rely on): a
+    queued host-to-device copy reads its source when it runs, a queued
+    device-to-host copy has not written its destination before the host
+    waits, an event orders both."""
+    assert simt.simt_selftest_defer() == 0
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_pinned_stage_simt(pkg, O, simt, monkeypatch, seed):
+    """Every host <-> HBM copy goes through the index's double-buffered pinned
+    stage (fmx_internal.hpp Stage).  With 4 KiB chunks the blob
+    upload and a 48 KB batch (2,400 x 20 bp) take many chunks in turn through
+    the two buffers, and the deferred streams run each copy late: a buffer
+    refilled before its previous copy ran, or a result read before its copy
+    ran, gives wrong answers here.  Counts, locations (forward and reversed)
+    and the caller's buffer unchanged, against the oracle."""
+    monkeypatch.setenv("FMX_STAGE_CHUNK", "4096")
+    simt.simt_config(900 + seed, 0.5)
+    simt.simt_defer(1, 0.5)
+    rng = np.random.default_rng(55 + seed)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=40_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
+    pats = [text[s:s + 20] for s in rng.integers(0, len(text) - 20, size=2_400)]
+    pats += [b"ACGTN" * 4, b"A" * 20]
+    data, offsets = pkg.pack_patterns(pats)
+    ref = data.copy()
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ooff, olocs = orc.locate_batch(data, offsets)
+    for occ in (0, 1):
+        ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=occ)
+        goff, glocs = ix.locate_batch((data, offsets))
+        assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+        assert np.array_equal(ix.count_batch((data, offsets)).astype(np.uint64), np.diff(ooff))
+        roff, rlocs = ix.locate_batch([p[::-1] for p in pats], reversed=True)
+        assert np.array_equal(roff, ooff) and np.array_equal(rlocs, olocs)
+        ix.close()
+    assert np.array_equal(data, ref), "the caller's pattern buffer changed"
+    simt.simt_defer(1, 0.25)
