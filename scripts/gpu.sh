@@ -24,6 +24,10 @@
 #   emitab   k_emit / k_group_tiles with 4 tiles per workgroup (this build) vs 1 (build_ab/libfmx_e1.so
 #            via FMX_LIB, built with -DFMX_EMIT_TILES=1), alternating twice
 #   gloo2    bench.py --gpus 2 over gloo on the one GPU (the multi-rank path: in-step gathers)
+#   c4presort  C4 at 8 and 256 batches per launch (launch order) and presorted by the last 3-6 residues
+#   c4group  C4 grouped (last 3 residues) with and without the refine pass, vs launch order, 256 per launch
+#   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
+#   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
 # Every step has its own time limit; the first failing step ends the run.
 # Output: gpurun_out/TAG/*.
 set -o pipefail
@@ -108,6 +112,28 @@ for step in "$@"; do
             FMX_LIB=$PWD/build_ab/libfmx_e1.so run emit_e1_c1 300 python -u bench.py --config c1 --no-cpu || exit 1
             run emit_e4_c1 300 python -u bench.py --config c1 --no-cpu || exit 1 ;;
         gloo2) FMX_BENCH_BACKEND=gloo run bench_gloo2 600 python -u bench.py --gpus 2 --no-cpu || exit 1 ;;
+        c4presort)  # C4 at 256 batches per launch in launch order, and the upper bound of sorting by the last L residues
+            B="python -u bench.py --config c4 --no-cpu --no-blob-layout --group 256"
+            run c4_g8 400 python -u bench.py --config c4 --no-cpu --no-blob-layout || exit 1
+            run c4_g256 400 $B || exit 1
+            for L in 3 4 5 6; do
+                run "c4_presort$L" 400 $B --presorted --presort-symbols $L || exit 1
+            done ;;
+        c4group)  # C4 grouped at 256 batches per launch: key = last 3 residues, + refine by the next 3
+            B="python -u bench.py --config c4 --no-blob-layout --group 256"
+            FMX_GROUPED=1 FMX_GROUP_REFINE_MIN=1 run c4_grouped_refine 500 $B || exit 1
+            FMX_GROUPED=1 run c4_grouped 500 $B --no-cpu || exit 1
+            run c4_g256_lo 500 $B --no-cpu || exit 1
+            FMX_GROUPED=1 FMX_GROUP_REFINE_MIN=1 run c4_grouped_refine2 500 $B --no-cpu || exit 1 ;;
+        rawab)  # C2 grouped with id-only records (no symbol decode in the place pass) vs packed, alternating
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "packed_$r" 300 $B || exit 1
+                FMX_GROUPED_RAW=1 run "raw_$r" 300 $B || exit 1
+            done ;;
+        singletrace)  # where one 100k batch per call spends its time
+            run single_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/single" -o run --output-format csv -- \
+                python3 -u bench.py --single-batch-only || exit 1 ;;
         trace)
             run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run --output-format csv -- \
                 python3 -u bench.py --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1

@@ -326,10 +326,14 @@ constexpr uint32_t kEmitTiles = FMX_EMIT_TILES;
 //   [256 B header][kGroupCounterRoom u32 key counters][tile counts: G][tile
 //   offsets: G][search records: n x R][its share of the sorted order: n x 16 B]
 // The counters sit at a fixed offset in batch 0's workspace; every grouped
-// launch zeroes them on its stream first (16 KB, a few microseconds), so no
+// launch zeroes them on its stream first (32 KB, a few microseconds), so no
 // launch depends on how an earlier one on the workspace ended.
 #ifndef FMX_GROUP_KEY_BITS
-#define FMX_GROUP_KEY_BITS 12  // (build option, A/B: 14 = 16,384 bins, C2 keys on 7 symbols)
+// 8,192 bins: DNA keys on its last 6 symbols (4,096 bins), a 20-residue
+// alphabet on its last 3 (8,000) — the k-mer seed's, after which the refine
+// pass orders each run by the next 3 (round 5).  (Build option, A/B: 12 was
+// the round-4 width; 14 = 16,384 bins, C2 keys on 7 symbols: slower, round 3.)
+#define FMX_GROUP_KEY_BITS 13
 #endif
 constexpr uint32_t kGroupKeyBits = FMX_GROUP_KEY_BITS;
 constexpr uint32_t kGroupBins = 1u << kGroupKeyBits;

@@ -787,9 +787,11 @@ __host__ __device__ constexpr uint32_t grouped_pat_bytes(uint32_t k, uint32_t ca
     return 256u * k * cap > kWsortBytes || !wsort ? 256u * k * cap : kWsortBytes;
 }
 
-// opts bit 0 (kGroupedXcd): the XCD deal below; opts >> 8 = wsort: a full
+// opts bit 0 (kGroupedXcd): the XCD deal below; bits 8-15 = wsort: a full
 // workgroup of packed records (K = 1) first sorts its 256 patterns by their
-// next wsort symbols after the key (digits over the key's base, the nearest
+// next wsort symbols after the first opts >> 16 last symbols — those the
+// sorted order is already ordered by: the key's, or with the refine pass
+// twice as many (digits over the key's base, the nearest
 // symbol most significant; base^wsort <= 256) — an LDS counting sort — so
 // that a wave's lanes share up to gkey_len + 1 or 2 last symbols and the LF
 // steps just below the key read the same lines in the same wave instruction
@@ -806,7 +808,8 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     __shared__ uint32_t s_vfirst[kMaxGroup];  // batch j's first pattern id (tile_begin * 256)
     __shared__ uint8_t s_dig[kMaxSigma + 1];  // (wsort) symbol -> digit; sigma (past the pattern's start) -> 0
     __shared__ uint64_t s_wscan[4];
-    const uint32_t wsort = K == 1 && !grp.graw ? opts >> 8 : 0u, xcd = opts & kGroupedXcd;
+    const uint32_t wsort = K == 1 && !grp.graw ? (opts >> 8) & 0xffu : 0u, xcd = opts & kGroupedXcd;
+    const uint32_t wskip = opts >> 16;
     FMX_DYN_LDS(s_pat);  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
     stage_tables(a, s, s_pat + grouped_pat_bytes(K, cap, wsort));
     if (threadIdx.x <= (uint32_t)kMaxSigma)
@@ -854,11 +857,11 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         if (K == 1 && wsort && (uint64_t)chunk * 256u + 256u <= total) {  // (workgroup-uniform: all lanes live)
             uint32_t *hist = reinterpret_cast<uint32_t *>(s_pat);
             U4 *stage = reinterpret_cast<U4 *>(s_pat + 1024);
-            const uint32_t t = threadIdx.x, L = grp.gkey_len, base = grp.gkey_base;
+            const uint32_t t = threadIdx.x, base = grp.gkey_base;
             const uint32_t m = sb[lds_upper(s_vfirst, grp.n, e.w)].stride;
             uint32_t k2 = 0;
             for (uint32_t d = 0; d < wsort; ++d) {
-                const uint32_t back = L + d;  // 0 = the pattern's last symbol
+                const uint32_t back = wskip + d;  // 0 = the pattern's last symbol
                 k2 = k2 * base + s_dig[back < m ? packed_sym(e, m - 1 - back, grp.gbits) : a.sigma];
             }
             hist[t] = 0;

@@ -383,7 +383,8 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     else
         hipLaunchKernelGGL((k_group_key<25, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (!raw && total >= ix->group_refine_min) {
+    const bool refined = !raw && total >= ix->group_refine_min;
+    if (refined) {
         // one workgroup per key from 4,096 patterns per key on average (C2's 25.6 M: every key its own)
         const uint32_t rg = (uint32_t)std::min<uint64_t>(kGroupBins, std::max<uint64_t>(1, total / 4096));
         hipLaunchKernelGGL(k_group_refine<0>, dim3(rg), dim3(1024), 0, stream, qa, grp, rb);
@@ -402,13 +403,14 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
     for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
     if (raw && cap > kGroupRawStage) cap = 4;
     // (two patterns per lane: packed records only — 512 lanes' staging would not fit LDS)
-    // the in-workgroup sort's symbols: as many after the key as base^w <= 256 allows (none when every
-    // pattern ends within the key)
+    // the in-workgroup sort's symbols: as many after those already in order (the key's, and the refine
+    // pass's as many again) as base^w <= 256 allows (none when every pattern ends within them)
+    const uint32_t sorted_len = grp.gkey_len * (refined ? 2u : 1u);
     uint32_t wsort = 0;
-    if (ix->grouped_wsort && !raw && !(ix->grouped_pair) && maxm > grp.gkey_len)
-        for (uint32_t w = 1, p = grp.gkey_base; p <= 256 && w <= 8 && w <= maxm - grp.gkey_len; ++w, p *= grp.gkey_base)
+    if (ix->grouped_wsort && !raw && !(ix->grouped_pair) && maxm > sorted_len)
+        for (uint32_t w = 1, p = grp.gkey_base; p <= 256 && w <= 8 && w <= maxm - sorted_len; ++w, p *= grp.gkey_base)
             wsort = w;
-    const uint32_t opts = (ix->grouped_xcd ? kGroupedXcd : 0u) | wsort << 8;
+    const uint32_t opts = (ix->grouped_xcd ? kGroupedXcd : 0u) | wsort << 8 | sorted_len << 16;
     if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair && !raw, opts,
                                    stream)) !=
         hipSuccess)

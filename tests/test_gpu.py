@@ -133,7 +133,8 @@ def check_parity(pkg, O, blob, pb, planes, vb, enc, pats, occ, reversed_too=True
     if expect_path is not None:
         info = ix.info()
         took = {k: info["launches_" + k] for k in ("grouped", "grouped_raw", "ordered")}
-        assert took[expect_path] >= 1, f"the locate did not run {expect_path}: {took}"
+        assert took[expect_path] >= 1 and sum(took.values()) == took[expect_path], \
+            f"the locate did not run {expect_path} alone: {took}"
     if not np.array_equal(goff, ooff):
         pytest.fail("per-pattern counts / offsets differ: " + diagnose(pkg, ix, load, data, offsets, pats, goff,
                                                                         ooff) + "; " + watch.report())

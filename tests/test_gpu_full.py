@@ -91,7 +91,10 @@ def run_config(pkg, O, n, alphabet, symbols, pos, planes, vec, m, npat, seed, ex
         goff, glocs = ix.locate_batch((pats, offsets))
         info = ix.info()
         took = {k: info["launches_" + k] for k in ("grouped", "grouped_raw", "ordered")}
-        assert took[path] == 1 and sum(took.values()) == 1, f"options {options} {env}: expected {path}, ran {took}"
+        # (one call may launch more than once: the host API reruns a batch whose locations overflow its
+        # first output guess)
+        assert took[path] >= 1 and sum(took.values()) == took[path], \
+            f"options {options} {env}: expected {path}, ran {took}"
         assert np.array_equal(goff, ooff), f"offsets differ, options {options} {env}"
         assert np.array_equal(glocs, olocs), f"locations differ, options {options} {env}"
         cnt = ix.count_batch((pats, offsets))

@@ -181,11 +181,12 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
 
 def test_default_policy_by_alphabet(pkg, O, monkeypatch):
     """Grouping is on by default where the key spans at least 5 symbols
-    (ACGT: 6) and off for a 20-residue alphabet (key of 2 symbols)."""
+    (ACGT: 6) and off for a 20-residue alphabet (key of 3 symbols: no LF
+    step beyond a k = 3 seed shared by the key alone)."""
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
     rng = np.random.default_rng(9)
-    for chars, want_len, on in ((b"ACGT", 6, True), (b"ACDEFGHIKLMNPQRSTVWY", 2, False)):
+    for chars, want_len, on in ((b"ACGT", 6, True), (b"ACDEFGHIKLMNPQRSTVWY", 3, False)):
         table = table_from_symbols([bytes([c]) for c in chars])
         text = rand_text(rng, chars, 20_000, 20_000)
         blob = T.gpu_build(pkg, text, len(chars), 4, 5, 64, 2, 2, table)

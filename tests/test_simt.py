@@ -217,7 +217,7 @@ def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb
     check_simt(pkg, O, blob, pb, planes, vb, pats, 1)
 
 
-GROUP_BINS = 4096  # fmx_internal.hpp kGroupBins: the key counters' 16 KiB
+GROUP_BINS = 8192  # fmx_internal.hpp kGroupBins: the key counters' 32 KiB
 
 
 def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
@@ -393,3 +393,31 @@ def test_pinned_stage_simt(pkg, O, simt, monkeypatch, seed):
         ix.close()
     assert np.array_equal(data, ref), "the caller's pattern buffer changed"
     simt.simt_defer(1, 0.25)
+
+
+@pytest.mark.parametrize("refine", ["1", "0"])
+def test_protein_grouped_refine_simt(pkg, O, simt, monkeypatch, refine):
+    """C4's shape (20 residues + X wildcard, sigma 21, u32/Block5<u64>): a
+    grouped launch keys on the last 3 residues (8,000 of the 8,192 bins), the
+    refine pass orders each key's run by the next 3, and the in-workgroup sort
+    then orders a workgroup by the residue after those 6 (or after the key's 3
+    without the refine pass); 3,000 x 12 aa + absent and X patterns, forward
+    and reversed, the sorted order checked on the device, against the
+    oracle."""
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
+    monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1" if refine == "1" else "18446744073709551615")
+    simt.simt_config(2121 + int(refine), 0.5)
+    rng = np.random.default_rng(21)
+    amino = b"ACDEFGHIKLMNPQRSTVWY"
+    table = table_from_symbols([bytes([c]) for c in amino] + [b"X"])
+    text = rng.choice(np.frombuffer(amino, np.uint8), size=30_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 21, O.layout(4, 5, 64), 3, 2, table)
+    pats = [text[s:s + 12] for s in rng.integers(0, len(text) - 12, size=3_000)]
+    pats += [bytes(rng.choice(np.frombuffer(amino, np.uint8), size=12)) for _ in range(50)]
+    pats += [b"X" * 12, b"W" * 12, text[:12], text[-12:]]
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block5(pkg.Vector.U64), options=1)
+    info = ix.info()
+    assert info["group_key_len"] == 3 and info["group_key_base"] == 20
+    ix.close()
+    check_simt(pkg, O, blob, 4, 5, 64, pats, 1)
