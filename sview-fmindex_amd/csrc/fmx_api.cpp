@@ -578,6 +578,10 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         ix->slots[idx].pinned = true;
         ix->slots[idx].inflight = 0;
     }
+    // the tables kernels read one entry per lane, in HBM (QueryTables; uploaded
+    // below, once dlut_dig is known — the record re-layout does not read them)
+    if (hipMalloc(&ix->d_tab, sizeof(QueryTables)) != hipSuccess) return FMX_E_DEVICE;
+    q.tab = ix->d_tab;
     // the k-mer count table (W^k entries of P) goes to LDS when it is small
     {
         const uint64_t ktb = v.kmer_len * v.L.pos_bytes;
@@ -625,6 +629,16 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
         }
     // grouped launches: the key's digits are these S symbols; as many of the
     // last symbols as fit kGroupBins bins (C2: 6 of ACGT; C4: 2 residues)
+    {
+        QueryTables t{};
+        memcpy(t.enc, q.enc, 256);
+        memcpy(t.dig, q.dlut_dig, sizeof(t.dig));
+        memcpy(t.C, q.C, sizeof(t.C));
+        memcpy(t.mult, q.mult, sizeof(t.mult));
+        if (ix->stage.h2d(ix->d_tab, &t, sizeof(t), ix->stream) != hipSuccess ||
+            hipStreamSynchronize(ix->stream) != hipSuccess)
+            return FMX_E_DEVICE;
+    }
     ix->gkey_base = S;
     ix->gkey_len = 0;
     if (S >= 2)
@@ -1033,6 +1047,7 @@ void fmx_free(fmx_index *ix) {
     if (ix->d_dlut) hipFree(ix->d_dlut);
     if (ix->d_safull) hipFree(ix->d_safull);
     if (ix->d_text) hipFree(ix->d_text);
+    if (ix->d_tab) hipFree(ix->d_tab);
     if (ix->d_status) hipFree(ix->d_status);
     if (ix->d_blob_owned) hipFree(ix->d_blob_owned);
     if (ix->stream) hipStreamDestroy(ix->stream);

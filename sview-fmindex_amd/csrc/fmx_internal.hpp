@@ -57,7 +57,21 @@ struct BlobSizes {
 };
 fmx_status blob_sizes(uint64_t n, uint32_t sigma, fmx_layout L, uint32_t k, uint32_t sr, BlobSizes *S);
 
-// Kernel arguments for the query kernels (passed by value; < 2 KB).
+// The per-symbol tables of QueryArgs that kernels read one entry per lane
+// (staging them into LDS), in HBM: a kernel argument lives in the kernarg
+// segment, where a per-lane (vector) load costs ~12 us per kernel while a
+// scalar load costs nothing measurable (scripts/micro/kernarg_cost.hip,
+// profiles/r5/r5g_*: 14.4 vs 2.6 us for a 98-workgroup kernel) — the same
+// tables read from HBM cost no more than the scalar path.  Filled at load.
+struct QueryTables {
+    uint8_t enc[256];
+    uint8_t dig[kMaxSigma];  // = QueryArgs::dlut_dig
+    uint64_t C[kMaxSigma + 1];
+    uint64_t mult[kMaxK];
+};
+
+// Kernel arguments for the query kernels (passed by value; < 2 KB).  Arrays
+// indexed per lane are read from `tab` (QueryTables), not from here.
 struct QueryArgs {
     const uint8_t *ckpt;      // rank_checkpoints [P; blocks_len * sigma]
     const uint8_t *blocks;    // blocks [BlockN<V>; blocks_len]
@@ -65,6 +79,7 @@ struct QueryArgs {
     const uint8_t *kmer;      // kmer_count_table [P; W^k]
     const uint8_t *occ;       // interleaved occ records (FMX_OCC_INTERLEAVED), else null
     uint32_t *status;         // latched device status bits
+    const QueryTables *tab;   // enc, dlut_dig, C, mult in HBM (per-lane reads)
     uint64_t n, sentinel;
     uint32_t sigma, k, sr, sr_pow2_mask;  // sr_pow2_mask = sr-1 if sr is a power of two, else 0
     uint32_t sr_pow2, sr_shift;          // sr is a power of two (1 included), log2(sr)
@@ -223,6 +238,7 @@ struct fmx_index {
     uint8_t *d_safull = nullptr;
     uint64_t safull_bytes = 0;
     uint8_t *d_text = nullptr;
+    fmx::QueryTables *d_tab = nullptr;
     uint32_t options = 0;
     fmx::QueryArgs qa{};
     // host-API scratch (grown on demand) and its private locate workspace

@@ -31,10 +31,11 @@ static inline unsigned grid_stride_for(uint64_t n) {
 template <typename P>
 __device__ __forceinline__ void stage_tables(const QueryArgs &a, Tables<P> &s, uint8_t *kt_lds) {
     const int t = threadIdx.x;
-    s.enc[t] = a.enc[t];
-    if (t < kMaxSigma) s.dig[t] = a.dlut_dig[t];
-    if ((uint32_t)t <= a.sigma) s.C[t] = (P)a.C[t];
-    if ((uint32_t)t < a.k) s.mult[t] = a.mult[t];
+    const QueryTables &g = *a.tab;
+    s.enc[t] = g.enc[t];
+    if (t < kMaxSigma) s.dig[t] = g.dig[t];
+    if ((uint32_t)t <= a.sigma) s.C[t] = (P)g.C[t];
+    if ((uint32_t)t < a.k) s.mult[t] = g.mult[t];
     if (a.kt_lds_bytes && kt_lds) {
         const uint32_t *src = reinterpret_cast<const uint32_t *>(a.kmer);
         uint32_t *dst = reinterpret_cast<uint32_t *>(kt_lds);
@@ -482,8 +483,8 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
         s_sorted[t] = group_sorted(grp.b[t], rec_bytes);
         s_first[t] = grp.b[t].first;
     }
-    if (t < 256) s_enc[t] = a.enc[t];
-    if (t < (uint32_t)kMaxSigma) s_dig[t] = a.dlut_dig[t] == kNoDigit ? 0 : a.dlut_dig[t];  // (absent: occurs nowhere)
+    if (t < 256) s_enc[t] = a.tab->enc[t];
+    if (t < (uint32_t)kMaxSigma) s_dig[t] = a.tab->dig[t] == kNoDigit ? 0 : a.tab->dig[t];  // (absent: occurs nowhere)
     if (t == 0) {
         uint32_t w = 1;
         for (uint32_t e = 0; e < 32; ++e) {
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(1024) void k_group_refine(const QueryArgs a, const 
         s_stride[t] = grp.b[t].stride;
     }
     const uint32_t sym_max = a.sigma, L = grp.gkey_len, bits = grp.gbits;
-    if (t <= (uint32_t)kMaxSigma) s_dig[t] = t < sym_max && a.dlut_dig[t] != kNoDigit ? a.dlut_dig[t] : 0;
+    if (t <= (uint32_t)kMaxSigma) s_dig[t] = t < sym_max && a.tab->dig[t] != kNoDigit ? a.tab->dig[t] : 0;
     if (t == 0) {
         uint32_t w = 1;
         for (uint32_t e = 0; e < 32; ++e) {
@@ -814,7 +815,7 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     stage_tables(a, s, s_pat + grouped_pat_bytes(K, cap, wsort));
     if (threadIdx.x <= (uint32_t)kMaxSigma)
         s_dig[threadIdx.x] =
-            threadIdx.x < a.sigma && a.dlut_dig[threadIdx.x] != kNoDigit ? a.dlut_dig[threadIdx.x] : 0;
+            threadIdx.x < a.sigma && a.tab->dig[threadIdx.x] != kNoDigit ? a.tab->dig[threadIdx.x] : 0;
     for (uint32_t j = threadIdx.x; j < grp.n; j += 256) {
         const LocateBatch &B = grp.b[j];
         const uint64_t G = (B.npat + 255) / 256;
@@ -989,7 +990,7 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
     const uint32_t fold = flags & 1u, narrow = flags & 2u;
     __shared__ P sC[kMaxSigma + 1];
     __shared__ uint64_t s_scan[E][4], s_part[4];
-    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.tab->C[threadIdx.x];
     const uint32_t jb = emit_batch(grp, blockIdx.x);
     const LocateBatch &B = grp.b[jb];
     const uint64_t npat = B.npat, G = (npat + 255) / 256;

@@ -156,8 +156,8 @@ __global__ __launch_bounds__(256) void k_group_check_order(const QueryArgs a, co
         s_first[j] = grp.b[j].first;
         s_vfirst[j] = grp.tile_begin[j] * 256u;
     }
-    s_enc[t] = a.enc[t];
-    if (t < (uint32_t)kMaxSigma) s_dig[t] = a.dlut_dig[t] == kNoDigit ? 0 : a.dlut_dig[t];
+    s_enc[t] = a.tab->enc[t];
+    if (t < (uint32_t)kMaxSigma) s_dig[t] = a.tab->dig[t] == kNoDigit ? 0 : a.tab->dig[t];
     if (t == 0) {
         uint32_t w = 1;
         for (uint32_t e = 0; e < 32; ++e) {
@@ -244,7 +244,7 @@ template <typename P>
 __global__ __launch_bounds__(256) void k_text(const QueryArgs a, uint64_t n, const P *__restrict__ sa,
                                               uint32_t stride, uint8_t *__restrict__ text) {
     __shared__ P sC[kMaxSigma + 1];
-    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.C[threadIdx.x];
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.tab->C[threadIdx.x];
     __syncthreads();
     for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (uint64_t)gridDim.x * 256) {
         uint32_t c = 0;
