@@ -26,6 +26,7 @@
 #   gloo2    bench.py --gpus 2 over gloo on the one GPU (the multi-rank path: in-step gathers)
 #   c4presort  C4 at 8 and 256 batches per launch (launch order) and presorted by the last 3-6 residues
 #   c4group  C4 grouped (last 3 residues) with and without the refine pass, vs launch order, 256 per launch
+#   c4rec    C4 with symbol-mask / paired-chunk / plain occ records (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0), twice
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
 # Every step has its own time limit; the first failing step ends the run.
@@ -125,6 +126,13 @@ for step in "$@"; do
             FMX_GROUPED=1 run c4_grouped 500 $B --no-cpu || exit 1
             run c4_g256_lo 500 $B --no-cpu || exit 1
             FMX_GROUPED=1 FMX_GROUP_REFINE_MIN=1 run c4_grouped_refine2 500 $B --no-cpu || exit 1 ;;
+        c4rec)  # C4's occ record encoding: symbol masks (3 lines per block, the default) vs paired chunks vs plain
+            B="python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "c4_masks_$r" 400 $B || exit 1
+                FMX_OCC_ONEHOT=0 run "c4_paired_$r" 400 $B || exit 1
+                FMX_OCC_ONEHOT=0 FMX_OCC_PAIRED=0 run "c4_plain_$r" 400 $B || exit 1
+            done ;;
         rawab)  # C2 grouped with id-only records (no symbol decode in the place pass) vs packed, alternating
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
             for r in 1 2; do

@@ -10,9 +10,11 @@
 //            QueryArgs::C: vector loads from the kernarg segment)
 //   table    the 26 KB struct in device memory, its pointer the argument
 // Each runs 2,000 times back to back on one stream; rocprofv3 --kernel-trace
-// --stats gives the per-kernel durations, hipEvents the per-launch wall.
+// --stats gives the per-kernel durations, hipEvents the per-launch wall, the
+// host clock around the launch loop the host's enqueue cost per launch.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -74,19 +76,23 @@ int main() {
     for (int rep = 0; rep < 2; ++rep)
         for (int k = 0; k < 4; ++k) {
             hipEventRecord(a, s);
+            const auto h0 = std::chrono::steady_clock::now();
             for (int it = 0; it < 2000; ++it) {
                 if (k == 0) hipLaunchKernelGGL(k_small, dim3(grid), dim3(256), 0, s, src, dst, grid * 256ull);
                 if (k == 1) hipLaunchKernelGGL(k_big_s, dim3(grid), dim3(256), 0, s, h);
                 if (k == 2) hipLaunchKernelGGL(k_big_v, dim3(grid), dim3(256), 0, s, h);
                 if (k == 3) hipLaunchKernelGGL(k_table, dim3(grid), dim3(256), 0, s, (const Big *)d_big);
             }
+            const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
             hipEventRecord(b, s);
             hipEventSynchronize(b);
             float ms = 0;
             hipEventElapsedTime(&ms, a, b);
             if (rep == 1)
-                printf("{\"kernel\": \"%s\", \"kernarg_bytes\": %zu, \"us_per_launch\": %.3f}\n", names[k],
-                       k == 0 ? sizeof(void *) * 3 : k == 3 ? sizeof(void *) : sizeof(Big), ms * 1e3 / 2000);
+                printf("{\"kernel\": \"%s\", \"kernarg_bytes\": %zu, \"us_per_launch\": %.3f, "
+                       "\"host_enqueue_us_per_launch\": %.3f}\n",
+                       names[k], k == 0 ? sizeof(void *) * 3 : k == 3 ? sizeof(void *) : sizeof(Big), ms * 1e3 / 2000,
+                       host_us / 2000);
         }
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
