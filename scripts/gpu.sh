@@ -27,6 +27,7 @@
 #   c4presort  C4 at 8 and 256 batches per launch (launch order) and presorted by the last 3-6 residues
 #   c4group  C4 grouped (last 3 residues) with and without the refine pass, vs launch order, 256 per launch
 #   c4rec    C4 with symbol-mask / paired-chunk / plain occ records (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0), twice
+#   launchab C1 on this build vs build_ab/libfmx_prev.so; single batch with 4 vs 1 tiles per k_emit workgroup
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
 # Every step has its own time limit; the first failing step ends the run.
@@ -132,6 +133,14 @@ for step in "$@"; do
                 run "c4_masks_$r" 400 $B || exit 1
                 FMX_OCC_ONEHOT=0 run "c4_paired_$r" 400 $B || exit 1
                 FMX_OCC_ONEHOT=0 FMX_OCC_PAIRED=0 run "c4_plain_$r" 400 $B || exit 1
+            done ;;
+        launchab)  # the launch path's host cost: this build vs build_ab/libfmx_prev.so (C1, launch-bound) and
+            # one tile per k_emit workgroup (build_ab/libfmx_e1.so) on the single-batch leg, alternating twice
+            for r in 1 2; do
+                run "c1_new_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
+                FMX_LIB=$PWD/build_ab/libfmx_prev.so run "c1_prev_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
+                run "single_e4_$r" 300 python -u bench.py --single-batch-only || exit 1
+                FMX_LIB=$PWD/build_ab/libfmx_e1.so run "single_e1_$r" 300 python -u bench.py --single-batch-only || exit 1
             done ;;
         rawab)  # C2 grouped with id-only records (no symbol decode in the place pass) vs packed, alternating
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"

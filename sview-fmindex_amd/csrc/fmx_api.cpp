@@ -1169,7 +1169,8 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
     // zero offset and total directly
     uint64_t i = 0;
     while (i < n_jobs) {
-        LocateGroup grp{};
+        LocateGroup grp;  // (the first grp.n entries are filled below; group_reset clears the rest that is read)
+        group_reset(grp);
         uint32_t stage = 0, tiles = 0;
         uint64_t units = 0;
         for (; i < n_jobs && grp.n < kMaxGroup; ++i) {

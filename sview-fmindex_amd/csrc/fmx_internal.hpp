@@ -312,8 +312,19 @@ struct LocateGroup {
     // zero between launches: k_emit resets it); null = one workgroup per tile
     uint32_t *tile_ctr;
 };
+// A LocateGroup ready to be filled: no batches, launch-order fields clear.
+// (Not zeroed as a whole: 25 KB per launch of host memset, and the kernels
+// read only the first n entries of each array.)
+inline void group_reset(LocateGroup &g) {
+    g.n = 0;
+    g.gcount = nullptr;
+    g.gkey_len = g.gkey_base = g.gbits = g.graw = 0;
+    g.gtotal = 0;
+    g.tile_ctr = nullptr;
+}
 // `mid` (optional): an event recorded between k_search and k_emit (timing).
-hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
+// Fills grp's per-launch fields (first, emit_begin, the grouped fields) in place.
+hipError_t launch_locate_group(const fmx_index *ix, LocateGroup &grp, uint32_t stage_flags,
                                uint32_t *status, hipStream_t stream, hipEvent_t mid = nullptr);
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.

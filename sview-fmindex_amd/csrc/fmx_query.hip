@@ -438,10 +438,9 @@ static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup &grp, boo
 }
 
 // The kernels of a (grouped) locate, one after another on `stream`.
-static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp_in, uint32_t tiles,
+static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
                                uint32_t sb, hipStream_t stream, hipEvent_t mid = nullptr) {
     const Disp d = dispatch(ix);
-    LocateGroup grp = grp_in;
     uint64_t total = 0;
     uint32_t ewg = 0;  // k_emit / k_group_tiles workgroups (kEmitTiles tiles of one batch each)
     for (uint32_t j = 0; j < grp.n; ++j) {
@@ -479,14 +478,16 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
     QueryArgs qa = ix->qa;
     qa.status = status;
     if ((n + 255) / 256 > tiles_cap || tiles_cap > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    LocateGroup grp{};
+    LocateGroup grp;
+    group_reset(grp);
+    grp.tile_begin[0] = 0;
     grp.b[0] = LocateBatch{d_bytes, d_offsets, n, d_counts, d_loc_offsets, d_locs, cap, d_needed, d_tiles,
                            (flags & FMX_PATTERN_REVERSED) ? 1u : 0u, flags >> 16};
     grp.n = 1;
     return launch_split(ix, qa, grp, (uint32_t)((n + 255) / 256), stage_bytes_for(flags), stream);
 }
 
-hipError_t launch_locate_group(const fmx_index *ix, const LocateGroup &grp, uint32_t stage_flags,
+hipError_t launch_locate_group(const fmx_index *ix, LocateGroup &grp, uint32_t stage_flags,
                                uint32_t *status, hipStream_t stream, hipEvent_t mid) {
     QueryArgs qa = ix->qa;
     qa.status = status;
