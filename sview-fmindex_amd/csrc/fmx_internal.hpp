@@ -295,7 +295,7 @@ struct LocateBatch {
 struct LocateGroup {
     LocateBatch b[kMaxGroup];
     uint32_t tile_begin[kMaxGroup];  // first workgroup of batch j (tile_begin[0] = 0)
-    uint32_t emit_begin[kMaxGroup];  // first k_emit / k_group_tiles workgroup of batch j (kEmitTiles tiles each)
+    uint32_t emit_begin[kMaxGroup];  // first k_group_tiles workgroup of batch j (kEmitTiles tiles each)
     uint32_t n;
     // Grouped launch (kWsHeader below): the group's key counters (batch 0's
     // workspace, zeroed on the launch's stream before its first kernel), the
@@ -329,10 +329,13 @@ hipError_t launch_locate_group(const fmx_index *ix, LocateGroup &grp, uint32_t s
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;
-// k_emit and k_group_tiles take this many tiles of one batch per workgroup:
-// each of their waves has that many record loads in flight instead of one
-// (a workgroup's life is mostly one HBM round trip; 100,000 one-tile
-// workgroups per C2 launch ran ~49 rounds of them).  Build option for A/B.
+// k_group_tiles takes this many tiles of one batch per workgroup: each of its
+// waves has that many record loads in flight instead of one (a workgroup's
+// life is mostly one HBM round trip; 121 -> 64 us per C2 launch at 4,
+// profiles/r4/r4k_*).  Build option for A/B.  k_emit takes one tile per
+// workgroup (its workgroups are the search's tiles: tile_begin): 4 did not
+// change it on the headline (227 us either way, r4k) and cost a lone 100k
+// batch 3.6 us (66.8 vs 70.4 us per call, profiles/r5/r5n_*).
 #ifndef FMX_EMIT_TILES
 #define FMX_EMIT_TILES 4
 #endif

@@ -962,7 +962,7 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
                 NarrowRec<P>{mode[q] == kHitOne ? rloc[q] : lo_r[q], (P)(hi_r[q] - lo_r[q])};
 }
 
-// This workgroup's batch of a k_emit / k_group_tiles launch (workgroup-uniform).
+// This workgroup's batch of a k_group_tiles launch (workgroup-uniform).
 __device__ __forceinline__ uint32_t emit_batch(const LocateGroup &grp, uint32_t w) {
     uint32_t lo = 0, hi = grp.n;
     while (hi - lo > 1) {
@@ -974,10 +974,9 @@ __device__ __forceinline__ uint32_t emit_batch(const LocateGroup &grp, uint32_t 
 }
 
 // 3. Output offsets (tile offset + in-tile scan) and every location, rows
-// dealt across each wave's lanes (emit_locations).  Workgroup w takes tiles
-// [E k, E k + E) of its batch (k = w - emit_begin, E = kEmitTiles): lane t
-// loads its pattern of each of them first, so a wave has E record loads in
-// flight, then answers them tile by tile.
+// dealt across each wave's lanes (emit_locations).  Workgroup w takes tile
+// w - tile_begin of its batch (E = 1 tile per workgroup; the code handles E
+// tiles, lane t loading its pattern of each first).
 // fold bit 0: batches of at most kFoldTiles tiles need no k_scan: each
 // workgroup sums the counts of the tiles before its first (all final:
 // k_search is done), then carries the base across its own, and the last tile
@@ -986,15 +985,15 @@ __device__ __forceinline__ uint32_t emit_batch(const LocateGroup &grp, uint32_t 
 
 template <typename P, int N, int VB, int REC>
 __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGroup grp, uint32_t flags) {
-    constexpr uint32_t E = kEmitTiles;
+    constexpr uint32_t E = 1;
     const uint32_t fold = flags & 1u, narrow = flags & 2u;
     __shared__ P sC[kMaxSigma + 1];
     __shared__ uint64_t s_scan[E][4], s_part[4];
     if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.tab->C[threadIdx.x];
-    const uint32_t jb = emit_batch(grp, blockIdx.x);
+    const uint32_t jb = group_batch(grp, blockIdx.x);
     const LocateBatch &B = grp.b[jb];
     const uint64_t npat = B.npat, G = (npat + 255) / 256;
-    const uint64_t g0 = (uint64_t)(blockIdx.x - grp.emit_begin[jb]) * E;
+    const uint64_t g0 = (uint64_t)(blockIdx.x - grp.tile_begin[jb]) * E;
     const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
     P lo[E], rloc[E];
     uint64_t mask[E], cnt[E];

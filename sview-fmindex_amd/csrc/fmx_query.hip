@@ -442,7 +442,7 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
                                uint32_t sb, hipStream_t stream, hipEvent_t mid = nullptr) {
     const Disp d = dispatch(ix);
     uint64_t total = 0;
-    uint32_t ewg = 0;  // k_emit / k_group_tiles workgroups (kEmitTiles tiles of one batch each)
+    uint32_t ewg = 0;  // k_group_tiles workgroups (kEmitTiles tiles of one batch each); k_emit: one per tile
     for (uint32_t j = 0; j < grp.n; ++j) {
         grp.b[j].first = total;
         total += grp.b[j].npat;
@@ -467,7 +467,7 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     // (k_emit's flags: bit 0 fold, bit 1 NarrowRec records from the grouped search)
-    return d.ops->emit(qa, d.vb, d.rec, grp, ewg, fold | (grouped ? 2u : 0u), stream);
+    return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold | (grouped ? 2u : 0u), stream);
 }
 
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
