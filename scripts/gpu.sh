@@ -28,6 +28,7 @@
 #   c4group  C4 grouped (last 3 residues) with and without the refine pass, vs launch order, 256 per launch
 #   c4rec    C4 with symbol-mask / paired-chunk / plain occ records (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0), twice
 #   launchab C1 on this build vs build_ab/libfmx_prev.so; single batch with 4 vs 1 tiles per k_emit workgroup
+#   c1sweep  C1 at 16 / 64 / 256 batches per launch x 2 / 8 streams (+ 256 in launch order)
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
 # Every step has its own time limit; the first failing step ends the run.
@@ -142,6 +143,14 @@ for step in "$@"; do
                 run "single_e4_$r" 300 python -u bench.py --single-batch-only || exit 1
                 FMX_LIB=$PWD/build_ab/libfmx_e1.so run "single_e1_$r" 300 python -u bench.py --single-batch-only || exit 1
             done ;;
+        c1sweep)  # C1 (1,000-pattern batches, launch-bound): batches per launch x streams beyond round 3's 8/16
+            for g in 16 64 256; do
+                for st in 2 8; do
+                    run "c1_g${g}_s${st}" 300 python -u bench.py --config c1 --no-cpu --group $g --streams $st || exit 1
+                done
+            done
+            FMX_GROUPED=0 run c1_g256_s2_lo 300 python -u bench.py --config c1 --no-cpu --group 256 --streams 2 || exit 1
+            run c1_g16_s8_again 300 python -u bench.py --config c1 --no-cpu --group 16 --streams 8 || exit 1 ;;
         rawab)  # C2 grouped with id-only records (no symbol decode in the place pass) vs packed, alternating
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
             for r in 1 2; do

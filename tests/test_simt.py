@@ -421,3 +421,35 @@ def test_protein_grouped_refine_simt(pkg, O, simt, monkeypatch, refine):
     assert info["group_key_len"] == 3 and info["group_key_base"] == 20
     ix.close()
     check_simt(pkg, O, blob, 4, 5, 64, pats, 1)
+
+
+def test_workspace_alignment_simt(pkg, O, simt):
+    """the grouped passes read and write a workspace as 16-B
+    vectors, so fmx_locate_batch_async and fmx_locate_group_async refuse a
+    workspace that is not 16-byte aligned (FMX_E_ARG) instead of issuing
+    misaligned vector accesses; the same workspace 16 bytes further on works."""
+    rng = np.random.default_rng(4)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=5_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    pats = [text[s:s + 10] for s in rng.integers(0, len(text) - 10, size=50)]
+    data, offsets = pkg.pack_patterns(pats)
+    n = len(pats)
+    ws_need = ix.locate_workspace_size(n)
+    raw = np.zeros(ws_need + 64, np.uint8)
+    base = raw.ctypes.data + (-raw.ctypes.data) % 16
+    loff, locs, need = np.zeros(n + 1, np.int64), np.zeros(4096, np.int32), np.zeros(1, np.int64)
+    args = (data.ctypes.data, offsets.ctypes.data, n, loff.ctypes.data, locs.ctypes.data, 4096, need.ctypes.data)
+    with pytest.raises(pkg.FmxError) as ei:
+        ix.locate_batch_async(*args, base + 8, ws_need)
+    assert ei.value.code == pkg._native.FMX_E_ARG
+    with pytest.raises(pkg.FmxError) as ei:
+        ix.locate_group_async(ix.job_queue([ix.locate_job(*args, base + 8, ws_need)]))
+    assert ei.value.code == pkg._native.FMX_E_ARG
+    ix.locate_batch_async(*args, base + 16, ws_need)
+    ix.sync()
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ooff, olocs = orc.locate_batch(data, offsets)
+    assert np.array_equal(loff.view(np.uint64), ooff) and np.array_equal(locs[:olocs.size].view(np.uint32), olocs)
+    ix.close()
