@@ -28,6 +28,7 @@
 #   c4group  C4 grouped (last 3 residues) with and without the refine pass, vs launch order, 256 per launch
 #   c4rec    C4 with symbol-mask / paired-chunk / plain occ records (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0), twice
 #   launchab C1 on this build vs build_ab/libfmx_prev.so; single batch with 4 vs 1 tiles per k_emit workgroup
+#   clitrace the sview-memory loader's stage times (FMX_LOAD_TRACE=1), warm
 #   c1sweep  C1 at 16 / 64 / 256 batches per launch x 2 / 8 streams (+ 256 in launch order)
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
@@ -143,6 +144,13 @@ for step in "$@"; do
                 run "single_e4_$r" 300 python -u bench.py --single-batch-only || exit 1
                 FMX_LIB=$PWD/build_ab/libfmx_e1.so run "single_e1_$r" 300 python -u bench.py --single-batch-only || exit 1
             done ;;
+        clitrace)  # the sview-memory load's stages (FMX_LOAD_TRACE=1): file -> host memory, host -> HBM (pinned stage)
+            D=$PWD/.fmx_cli; rm -rf "$D"; mkdir -p "$D"; CLI="python sview-fmindex_amd/bench_cli.py"
+            run clitrace_generate 420 bash -c "$CLI generate-text -d $D -t 1000000000 -s 7 && \
+                $CLI generate-pattern -d $D -p 20 -n 100000 -s 7 && $CLI build -d $D -a all -s 2 -k 3" || exit 1
+            FMX_LOAD_TRACE=1 run clitrace_locate 600 bash -c "$CLI locate -d $D -a sview-memory && \
+                $CLI locate -d $D -a sview-memory && $CLI locate -d $D -a sview-mmap" || exit 1
+            rm -rf "$D" ;;
         c1sweep)  # C1 (1,000-pattern batches, launch-bound): batches per launch x streams beyond round 3's 8/16
             for g in 16 64 256; do
                 for st in 2 8; do
