@@ -77,10 +77,11 @@ ACGTN = [b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"]
 AMINO = b"ACDEFGHIKLMNPQRSTVWY"
 CONFIGS = {
     # BASELINE.json configs[0]: the reference's CPU-runnable plumbing case (T is the wildcard)
-    # (1,000-pattern batches: launch-bound, so 16 batches per launch and 8 streams in flight —
-    # 1.46e9 vs 0.66e9 at 8 x 2, profiles/r3/r3c1_sweep.txt)
+    # (1,000-pattern batches: launch-bound below ~64 batches per launch; 256 per launch on 2 streams in
+    # launch order runs 8.17e9 vs 1.1e9 at round 3's 16 x 8 — the 1 Mbp index lives in cache, so the
+    # engine does not group it; profiles/r5/r5p_*)
     "c1": dict(text_len=1_000_000, alphabet=b"ACGT", symbols=[b"Aa", b"Cc", b"Gg", b"Tt"], pos=4, planes=2,
-               vec=64, k=3, sr=2, patterns=1_000, m=20, total=0, group=16, streams=8,
+               vec=64, k=3, sr=2, patterns=1_000, m=20, total=0, group=256, streams=2,
                desc="C1: 1 Mbp ACGT, 1,000 x 20 bp, u32/Block2<u64>, sr 2, k 3"),
     # configs[1]: the headline (metric quoted on it).  256 batches per launch (one launch group
     # per stream, 512 distinct batches): a grouped launch of 25.6 M patterns shares more of its

@@ -29,6 +29,8 @@
 #   c4rec    C4 with symbol-mask / paired-chunk / plain occ records (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0), twice
 #   launchab C1 on this build vs build_ab/libfmx_prev.so; single batch with 4 vs 1 tiles per k_emit workgroup
 #   clitrace the sview-memory loader's stage times (FMX_LOAD_TRACE=1), warm
+#   sizesweep  C2's shape on 100 / 250 / 500 Mbp texts, grouped vs launch order (the grouping size floor)
+#   c1streams  C1 at its default 256 batches per launch on 2 / 4 / 8 streams
 #   c1sweep  C1 at 16 / 64 / 256 batches per launch x 2 / 8 streams (+ 256 in launch order)
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
@@ -151,6 +153,16 @@ for step in "$@"; do
             FMX_LOAD_TRACE=1 run clitrace_locate 600 bash -c "$CLI locate -d $D -a sview-memory && \
                 $CLI locate -d $D -a sview-memory && $CLI locate -d $D -a sview-mmap" || exit 1
             rm -rf "$D" ;;
+        sizesweep)  # where grouping starts to pay: C2's shape on 100 / 250 / 500 Mbp texts, grouped vs launch order
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for n in 100000000 250000000 500000000; do
+                FMX_GROUPED=1 run "size_${n}_grouped" 300 $B --text-len $n || exit 1
+                FMX_GROUPED=0 run "size_${n}_lo" 300 $B --text-len $n || exit 1
+            done ;;
+        c1streams)  # C1's new default shape (256 batches per launch, launch order) on 2 / 4 / 8 streams
+            for st in 2 4 8; do
+                run "c1_s${st}" 300 python -u bench.py --config c1 --no-cpu --streams $st || exit 1
+            done ;;
         c1sweep)  # C1 (1,000-pattern batches, launch-bound): batches per launch x streams beyond round 3's 8/16
             for g in 16 64 256; do
                 for st in 2 8; do

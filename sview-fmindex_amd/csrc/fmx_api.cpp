@@ -430,7 +430,8 @@ static void host_copy(void *dst, const void *src, uint64_t n) {
         memcpy(dst, src, n);
         return;
     }
-    const unsigned nt = (unsigned)std::min<uint64_t>(4, n / (kPar / 2));
+    // up to 8 threads of >= 4 MiB each (a 2.7 GB blob: 88 ms host -> HBM with 4, r5p)
+    const unsigned nt = (unsigned)std::min<uint64_t>(8, n / (4ull << 20));
     const uint64_t part = (n / nt + 4095) & ~4095ull;
     std::vector<std::thread> th;
     uint64_t o = part;
@@ -644,9 +645,21 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (S >= 2)
         for (uint64_t bins = S; bins <= kGroupBins && ix->gkey_len < 16; bins *= S) ++ix->gkey_len;
     // on by default for launches of at least 131,072 patterns whose key spans
-    // at least 5 symbols (DNA: 6; a 20-residue alphabet keys on 2 only and
-    // shares too little): DESIGN.md §5, "Grouped launches"
-    ix->grouped_min = ix->gkey_len >= 5 ? 131072 : ~0ull;
+    // at least 5 symbols (DNA: 6; a 20-residue alphabet keys on 3, no more
+    // than its k-mer seed, and loses: DESIGN.md §5), on an index whose occ
+    // structure outgrows the 256 MiB Infinity Cache: a smaller one's lines
+    // hit in cache for every pattern anyway, and dealing out is pure cost
+    // (C1, 1 Mbp: 8.17 x 10^9 in launch order vs 4.2 grouped at 256 batches
+    // per launch; C2, 1 Gbp: grouped +38 %; profiles/r5/r5p_*).
+    // FMX_GROUPED_INDEX_MB moves that size.
+    {
+        const uint64_t occ = ix->occ_mode == FMX_OCC_INTERLEAVED
+                                 ? ix->occ_bytes
+                                 : v.ckpt_len * v.L.pos_bytes + v.blocks_len * v.block_bytes;
+        uint64_t floor = 256ull << 20;
+        if (const char *e = getenv("FMX_GROUPED_INDEX_MB")) floor = strtoull(e, nullptr, 10) << 20;
+        ix->grouped_min = ix->gkey_len >= 5 && occ >= floor ? 131072 : ~0ull;
+    }
     if (const char *e = getenv("FMX_GROUPED")) {
         if (e[0] == '0') ix->grouped_min = ~0ull;
         else if (e[0] == '1') ix->grouped_min = 1;

@@ -156,6 +156,12 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
     res = {}
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
+    monkeypatch.delenv("FMX_GROUPED_INDEX_MB", raising=False)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    # a 4 Mbp index fits the Infinity Cache: not grouped by default
+    assert ix.info()["grouped_min"] == 2 ** 64 - 1
+    ix.close()
+    monkeypatch.setenv("FMX_GROUPED_INDEX_MB", "0")  # (the size rule off: the alphabet rule alone)
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
     assert ix.info()["grouped_min"] == 131072  # the default for a key of at least 5 symbols
     ix.close()
@@ -182,9 +188,11 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
 def test_default_policy_by_alphabet(pkg, O, monkeypatch):
     """Grouping is on by default where the key spans at least 5 symbols
     (ACGT: 6) and off for a 20-residue alphabet (key of 3 symbols: no LF
-    step beyond a k = 3 seed shared by the key alone)."""
+    step beyond a k = 3 seed shared by the key alone) — on an index larger
+    than the Infinity Cache (FMX_GROUPED_INDEX_MB=0 here: these are small)."""
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
+    monkeypatch.setenv("FMX_GROUPED_INDEX_MB", "0")
     rng = np.random.default_rng(9)
     for chars, want_len, on in ((b"ACGT", 6, True), (b"ACDEFGHIKLMNPQRSTVWY", 3, False)):
         table = table_from_symbols([bytes([c]) for c in chars])

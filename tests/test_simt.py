@@ -453,3 +453,29 @@ def test_workspace_alignment_simt(pkg, O, simt):
     ooff, olocs = orc.locate_batch(data, offsets)
     assert np.array_equal(loff.view(np.uint64), ooff) and np.array_equal(locs[:olocs.size].view(np.uint32), olocs)
     ix.close()
+
+
+def test_grouping_policy_by_index_size_simt(pkg, O, simt, monkeypatch):
+    """The default grouping policy (fmx_api.cpp finish_load): a DNA index
+    whose occ structure fits the 256 MiB Infinity Cache is not grouped by
+    default (its lines hit in cache in any order: C1), the same index with
+    the size floor lowered (FMX_GROUPED_INDEX_MB) is, from 131,072 patterns
+    per launch; FMX_GROUPED=1 groups whatever the size."""
+    for k in ("FMX_GROUPED", "FMX_GROUPED_MIN", "FMX_GROUPED_INDEX_MB"):
+        monkeypatch.delenv(k, raising=False)
+    rng = np.random.default_rng(12)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=5_000).astype(np.uint8).tobytes()
+    blob = O.build(text, 5, O.layout(4, 3, 64), 3, 2, table)
+
+    def policy():
+        ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+        i = ix.info()
+        ix.close()
+        return i["group_key_len"], i["grouped_min"]
+    assert policy() == (6, 2 ** 64 - 1)
+    monkeypatch.setenv("FMX_GROUPED_INDEX_MB", "0")
+    assert policy() == (6, 131072)
+    monkeypatch.delenv("FMX_GROUPED_INDEX_MB")
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    assert policy() == (6, 1)
