@@ -155,7 +155,7 @@ for step in "$@"; do
             rm -rf "$D" ;;
         sizesweep)  # where grouping starts to pay: C2's shape on 100 / 250 / 500 Mbp texts, grouped vs launch order
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
-            for n in 100000000 250000000 500000000; do
+            for n in ${SIZES:-100000000 250000000 500000000}; do
                 FMX_GROUPED=1 run "size_${n}_grouped" 300 $B --text-len $n || exit 1
                 FMX_GROUPED=0 run "size_${n}_lo" 300 $B --text-len $n || exit 1
             done ;;

@@ -644,22 +644,15 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     ix->gkey_len = 0;
     if (S >= 2)
         for (uint64_t bins = S; bins <= kGroupBins && ix->gkey_len < 16; bins *= S) ++ix->gkey_len;
-    // on by default for launches of at least 131,072 patterns whose key spans
-    // at least 5 symbols (DNA: 6; a 20-residue alphabet keys on 3, no more
-    // than its k-mer seed, and loses: DESIGN.md §5), on an index whose occ
-    // structure outgrows the 256 MiB Infinity Cache: a smaller one's lines
-    // hit in cache for every pattern anyway, and dealing out is pure cost
-    // (C1, 1 Mbp: 8.17 x 10^9 in launch order vs 4.2 grouped at 256 batches
-    // per launch; C2, 1 Gbp: grouped +38 %; profiles/r5/r5p_*).
-    // FMX_GROUPED_INDEX_MB moves that size.
-    {
-        const uint64_t occ = ix->occ_mode == FMX_OCC_INTERLEAVED
-                                 ? ix->occ_bytes
-                                 : v.ckpt_len * v.L.pos_bytes + v.blocks_len * v.block_bytes;
-        uint64_t floor = 256ull << 20;
-        if (const char *e = getenv("FMX_GROUPED_INDEX_MB")) floor = strtoull(e, nullptr, 10) << 20;
-        ix->grouped_min = ix->gkey_len >= 5 && occ >= floor ? 131072 : ~0ull;
-    }
+    // on by default for launches of at least 2^20 patterns whose key spans at
+    // least 5 symbols (DNA: 6; a 20-residue alphabet keys on 3, no more than
+    // its k-mer seed, and loses: DESIGN.md §5).  Below ~1 M patterns the
+    // dealing out's fixed cost eats the sharing: at 256 batches of 1,000 (C1)
+    // launch order runs 8.0 vs 4.2 x 10^9 grouped (profiles/r5/r5p_*, r5q_*),
+    // at 0.8 M patterns on 1 Gbp the two were equal and at 1.6 M grouping
+    // gained 6 % (round 3); at 25.6 M patterns it gains 4 % on a 4 Mbp text
+    // and 50 % from 16 Mbp up (r5q_size_*, r5r_size_*).
+    ix->grouped_min = ix->gkey_len >= 5 ? (1ull << 20) : ~0ull;
     if (const char *e = getenv("FMX_GROUPED")) {
         if (e[0] == '0') ix->grouped_min = ~0ull;
         else if (e[0] == '1') ix->grouped_min = 1;

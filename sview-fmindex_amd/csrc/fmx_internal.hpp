@@ -209,7 +209,7 @@ struct fmx_index {
     bool status_pressure = false;  // most words assigned: launches record completion events
     bool search_persistent = false;  // FMX_SEARCH_PERSISTENT=1: k_search on a resident-sized grid (A/B)
     // grouped launches (fmx::kWsHeader): launches of at least grouped_min
-    // patterns on the faithful index — by default 131,072 when the key spans
+    // patterns on the faithful index — by default 2^20 when the key spans
     // at least 5 symbols (finish_load), FMX_GROUPED_MIN sets it, FMX_GROUPED=1
     // groups every launch that can be, FMX_GROUPED=0 none; the key = the last
     // gkey_len symbols, digits over the gkey_base symbols that occur in the text

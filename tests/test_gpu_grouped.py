@@ -1,7 +1,7 @@
 """Grouped launches (fmx_internal.hpp kWsHeader): a launch's
 patterns searched in the order of their last symbols instead of the order
 given.  A launch is grouped when its batches are fixed-length with
-patterns that pack into 96 bits (by default from 131,072 patterns, with a key
+patterns that pack into 96 bits (by default from 2^20 patterns, with a key
 of at least 5 symbols); FMX_GROUPED=1 groups every such launch, however
 small, so the parity tests below run the key / sorted-order / grouped-search
 / count kernels on fixed-length batches of every layout and alphabet size,
@@ -143,7 +143,7 @@ def test_out_of_alphabet_grouped(pkg, O, grouped):
 
 def test_grouped_equals_launch_order(pkg, O, monkeypatch):
     """A 300k-pattern fixed-length launch on a 4 Mbp text grouped (the
-    default above 131,072 patterns; FMX_GROUPED_MIN moves the threshold)
+    default from 2^20 patterns; FMX_GROUPED_MIN moves the threshold)
     answers exactly like the same launch in launch order (FMX_GROUPED=0), and
     like the oracle; the index reports the grouping it applies."""
     rng = np.random.default_rng(5)
@@ -156,14 +156,8 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
     res = {}
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
-    monkeypatch.delenv("FMX_GROUPED_INDEX_MB", raising=False)
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
-    # a 4 Mbp index fits the Infinity Cache: not grouped by default
-    assert ix.info()["grouped_min"] == 2 ** 64 - 1
-    ix.close()
-    monkeypatch.setenv("FMX_GROUPED_INDEX_MB", "0")  # (the size rule off: the alphabet rule alone)
-    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
-    assert ix.info()["grouped_min"] == 131072  # the default for a key of at least 5 symbols
+    assert ix.info()["grouped_min"] == 1 << 20  # the default for a key of at least 5 symbols
     ix.close()
     monkeypatch.setenv("FMX_GROUPED", "0")
     for mode in ("0", None):
@@ -186,13 +180,12 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
 
 
 def test_default_policy_by_alphabet(pkg, O, monkeypatch):
-    """Grouping is on by default where the key spans at least 5 symbols
-    (ACGT: 6) and off for a 20-residue alphabet (key of 3 symbols: no LF
-    step beyond a k = 3 seed shared by the key alone) — on an index larger
-    than the Infinity Cache (FMX_GROUPED_INDEX_MB=0 here: these are small)."""
+    """Grouping is on by default (launches of at least 2^20 patterns) where
+    the key spans at least 5 symbols (ACGT: 6) and off for a 20-residue
+    alphabet (key of 3 symbols: no LF step beyond a k = 3 seed shared by the
+    key alone)."""
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
-    monkeypatch.setenv("FMX_GROUPED_INDEX_MB", "0")
     rng = np.random.default_rng(9)
     for chars, want_len, on in ((b"ACGT", 6, True), (b"ACDEFGHIKLMNPQRSTVWY", 3, False)):
         table = table_from_symbols([bytes([c]) for c in chars])
@@ -201,7 +194,7 @@ def test_default_policy_by_alphabet(pkg, O, monkeypatch):
         ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block5(pkg.Vector.U64), options=1)
         info = ix.info()
         assert info["group_key_len"] == want_len and info["group_key_base"] == len(chars)
-        assert (info["grouped_min"] == 131072) == on
+        assert (info["grouped_min"] == 1 << 20) == on
         ix.close()
 
 

@@ -455,13 +455,14 @@ def test_workspace_alignment_simt(pkg, O, simt):
     ix.close()
 
 
-def test_grouping_policy_by_index_size_simt(pkg, O, simt, monkeypatch):
+def test_grouping_policy_simt(pkg, O, simt, monkeypatch):
     """The default grouping policy (fmx_api.cpp finish_load): a DNA index
-    whose occ structure fits the 256 MiB Infinity Cache is not grouped by
-    default (its lines hit in cache in any order: C1), the same index with
-    the size floor lowered (FMX_GROUPED_INDEX_MB) is, from 131,072 patterns
-    per launch; FMX_GROUPED=1 groups whatever the size."""
-    for k in ("FMX_GROUPED", "FMX_GROUPED_MIN", "FMX_GROUPED_INDEX_MB"):
+    (key of 6 symbols) groups launches of at least 2^20 patterns — below
+    that the dealing out's fixed cost eats the sharing (C1's 256 x 1,000
+    patterns: 8.0 vs 4.2 x 10^9 in launch order, profiles/r5/r5q_*);
+    FMX_GROUPED_MIN moves the threshold, FMX_GROUPED=1 groups every launch
+    that can be, FMX_GROUPED=0 none."""
+    for k in ("FMX_GROUPED", "FMX_GROUPED_MIN"):
         monkeypatch.delenv(k, raising=False)
     rng = np.random.default_rng(12)
     table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
@@ -473,9 +474,11 @@ def test_grouping_policy_by_index_size_simt(pkg, O, simt, monkeypatch):
         i = ix.info()
         ix.close()
         return i["group_key_len"], i["grouped_min"]
-    assert policy() == (6, 2 ** 64 - 1)
-    monkeypatch.setenv("FMX_GROUPED_INDEX_MB", "0")
-    assert policy() == (6, 131072)
-    monkeypatch.delenv("FMX_GROUPED_INDEX_MB")
+    assert policy() == (6, 1 << 20)
+    monkeypatch.setenv("FMX_GROUPED_MIN", "5000")
+    assert policy() == (6, 5000)
+    monkeypatch.delenv("FMX_GROUPED_MIN")
     monkeypatch.setenv("FMX_GROUPED", "1")
     assert policy() == (6, 1)
+    monkeypatch.setenv("FMX_GROUPED", "0")
+    assert policy() == (6, 2 ** 64 - 1)
