@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 6u
+#define FMX_ABI_VERSION 7u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -145,7 +145,9 @@ typedef struct fmx_index_info {
     uint64_t launches_grouped;      /* locate launches of this index so far, by the
                                        path they took: grouped with packed records, */
     uint64_t launches_grouped_raw;  /* grouped with id-only records,                  */
-    uint64_t launches_ordered;      /* in launch order (k_search)                     */
+    uint64_t launches_ordered;      /* in launch order,                               */
+    uint64_t launches_fused;        /* of those, as one kernel (k_locate: search,
+                                       offsets and locations; FMX_FUSED=0: never)   */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {

@@ -34,6 +34,9 @@
 #   c1sweep  C1 at 16 / 64 / 256 batches per launch x 2 / 8 streams (+ 256 in launch order)
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
+#   fusedtest  only tests/test_gpu_fused.py (the fused launch, k_locate)
+#   fusedab  the fused launch vs the two-kernel path (FMX_FUSED=0): single batch, C1, C4, alternating twice;
+#            then the single-batch kernel trace of the fused build
 # Every step has its own time limit; the first failing step ends the run.
 # Output: gpurun_out/TAG/*.
 set -o pipefail
@@ -177,6 +180,20 @@ for step in "$@"; do
                 run "packed_$r" 300 $B || exit 1
                 FMX_GROUPED_RAW=1 run "raw_$r" 300 $B || exit 1
             done ;;
+        fusedtest) run pytest_fused 600 python -u -m pytest tests/test_gpu_fused.py -x -v --timeout 300 \
+                --timeout-method thread || exit 1 ;;
+        fusedab)
+            for r in 1 2; do
+                run "single_fused_$r" 300 python -u bench.py --single-batch-only || exit 1
+                FMX_FUSED=0 run "single_split_$r" 300 python -u bench.py --single-batch-only || exit 1
+                run "c1_fused_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
+                FMX_FUSED=0 run "c1_split_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
+                run "c4_fused_$r" 400 python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch || exit 1
+                FMX_FUSED=0 run "c4_split_$r" 400 python -u bench.py --config c4 --no-cpu --no-blob-layout \
+                    --no-single-batch || exit 1
+            done
+            run single_trace_fused 400 rocprofv3 --kernel-trace --stats -d "$OUT/single" -o run --output-format csv -- \
+                python3 -u bench.py --single-batch-only || exit 1 ;;
         singletrace)  # where one 100k batch per call spends its time
             run single_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/single" -o run --output-format csv -- \
                 python3 -u bench.py --single-batch-only || exit 1 ;;

@@ -571,6 +571,17 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
     ix->slots.assign(kStatusSlots, StatusSlot{});
     if (const char *e = getenv("FMX_SEARCH_PERSISTENT")) ix->search_persistent = e[0] == '1';
+    // the fused launch (k_locate) and the bound on its waits: 4 s of the wall clock by default
+    if (const char *e = getenv("FMX_FUSED")) ix->fused = e[0] != '0';
+    if (const char *e = getenv("FMX_FUSED_MAX_TILES")) ix->fused_max_tiles = strtoull(e, nullptr, 0);
+    {
+        uint64_t ms = 4000;
+        if (const char *e = getenv("FMX_FUSED_TIMEOUT_MS")) ms = std::max<uint64_t>(1, strtoull(e, nullptr, 0));
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ix->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        ix->fused_late_ticks = ms * (uint64_t)khz;
+    }
     for (uint32_t i = kStatusSlots; i-- > 0;) ix->free_slots.push_back(i);
     {
         int idx = -1;
@@ -764,11 +775,13 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
     if (st & kStatusStride) return FMX_E_ARG;
-    if (st & (kStatusGroup | kStatusCheck)) {
+    if (st & (kStatusGroup | kStatusCheck | kStatusLate)) {
         static const bool debug = getenv("FMX_DEBUG") != nullptr;
         if (debug)
-            fprintf(stderr, "fmx: grouped launch: %s\n",
-                    (st & kStatusCheck) ? "sorted order failed FMX_GROUP_CHECK" : "sorted position out of range");
+            fprintf(stderr, "fmx: %s\n",
+                    (st & kStatusLate)    ? "fused launch: an earlier tile's count was not published in time"
+                    : (st & kStatusCheck) ? "grouped launch: sorted order failed FMX_GROUP_CHECK"
+                                          : "grouped launch: sorted position out of range");
         return FMX_E_DEVICE;
     }
     return FMX_OK;
@@ -1090,6 +1103,7 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->launches_grouped = ix->launches_grouped.load();
     o->launches_grouped_raw = ix->launches_grouped_raw.load();
     o->launches_ordered = ix->launches_ordered.load();
+    o->launches_fused = ix->launches_fused.load();
     o->device = ix->device;
     return FMX_OK;
 }

@@ -117,6 +117,7 @@ constexpr uint32_t kStatusSymbol = 2u;
 constexpr uint32_t kStatusStride = 8u;  // FMX_HINT_FIXED_LEN given, offsets disagree
 constexpr uint32_t kStatusGroup = 16u;  // a grouped launch's sorted position out of range (never expected)
 constexpr uint32_t kStatusCheck = 32u;  // FMX_GROUP_CHECK=1: a grouped launch's sorted order failed its check
+constexpr uint32_t kStatusLate = 64u;   // k_locate: an earlier tile's count not published in time (never expected)
 
 // One bracketed launch: events a -> b on its stream, and for a split locate
 // launch m between its two phases; timers[0] gets a -> b, timers[1] a -> m
@@ -232,6 +233,14 @@ struct fmx_index {
     // FMX_GROUP_CHECK=1 (debug): every grouped launch checks its sorted order before the search —
     // each pattern placed exactly once, under its own key, with its own symbols (k_group_check_*)
     bool group_check = false;
+    // launches in launch order run as one kernel (k_locate: search, then offsets and locations) when
+    // every batch has at most kFoldTiles tiles, the fixed-length hint and patterns of at most
+    // kFusedMaxLen symbols, and the launch has at most fused_max_tiles tiles (FMX_FUSED=0: never;
+    // FMX_FUSED_MAX_TILES); fused_late_ticks bounds its waits (FMX_FUSED_TIMEOUT_MS, 100 MHz ticks)
+    bool fused = true;
+    uint64_t fused_max_tiles = ~0ull;
+    uint64_t fused_late_ticks = 0;
+    mutable std::atomic<uint64_t> launches_fused{0};  // (a subset of launches_ordered)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -329,6 +338,10 @@ hipError_t launch_locate_group(const fmx_index *ix, LocateGroup &grp, uint32_t s
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;
+// k_locate (the fused launch) only for patterns up to this long: a tile's
+// search, which later tiles of its batch wait for, stays far below the wait
+// bound (fmx_index::fused_late_ticks).
+constexpr uint32_t kFusedMaxLen = 4096;
 // k_group_tiles takes this many tiles of one batch per workgroup: each of its
 // waves has that many record loads in flight instead of one (a workgroup's
 // life is mostly one HBM round trip; 121 -> 64 us per C2 launch at 4,
@@ -398,6 +411,9 @@ struct LayoutOps {
                           uint32_t stride, hipStream_t s);
     hipError_t (*relayout)(const QueryArgs &qa, uint32_t vb, uint32_t rec, uint64_t blocks_len, uint8_t *occ,
                            hipStream_t s);
+    // launch order as one kernel (k_locate): tag = the launch's hand-off tag, late_ticks its wait bound
+    hipError_t (*locate)(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const LocateGroup &grp,
+                         uint32_t tiles, uint32_t sb, uint64_t tag, uint64_t late_ticks, hipStream_t s);
 };
 uint64_t locate_tiles_cap(uint64_t n);
 // Bytes per pattern of the search-result records in the locate workspace.

@@ -166,6 +166,26 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
     });
 }
 
+[[maybe_unused]] hipError_t op_locate(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const LocateGroup &grp,
+                                      uint32_t tiles, uint32_t sb, uint64_t tag, uint64_t late_ticks, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        const uint32_t lds = sb + qa.kt_lds_bytes;
+        if (var == kVarFaithful) {
+            hipLaunchKernelGGL((k_locate<P, N, VB, R, kVarFaithful>), dim3(tiles), dim3(256), lds, s, qa, grp, sb, tag,
+                               late_ticks);
+        } else if constexpr (faithful_only(R)) {
+            return hipErrorInvalidValue;
+        } else if (var == kVarDerived) {
+            hipLaunchKernelGGL((k_locate<P, N, VB, R, kVarDerived>), dim3(tiles), dim3(256), lds, s, qa, grp, sb, tag,
+                               late_ticks);
+        } else {
+            hipLaunchKernelGGL((k_locate<P, N, VB, R, kVarDerivedLong>), dim3(tiles), dim3(256), lds, s, qa, grp, sb,
+                               tag, late_ticks);
+        }
+        return hipGetLastError();
+    });
+}
+
 }  // namespace
 
 #if !defined(__HIP_DEVICE_COMPILE__)  // a host table (the device pass only instantiates the kernels)
@@ -173,7 +193,7 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 #define FMX_OPS_NAME(p, n, v) FMX_OPS_NAME2(p, n, v)
 extern const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB);
 const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB) = {op_count, op_search, op_emit, op_search_grouped,
-                                                           op_dlut_level, op_full_sa, op_relayout};
+                                                           op_dlut_level, op_full_sa, op_relayout, op_locate};
 #endif
 
 }  // namespace fmx

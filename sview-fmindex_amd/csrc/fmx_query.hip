@@ -22,7 +22,10 @@
 // gathers, so the kernels keep many independent chains (lanes) in flight and
 // make each LF step cost one record read per rank query — one for both when
 // lo and hi share a block.
+#include <atomic>
+#include <chrono>
 #include <cstring>
+#include <random>
 
 #include "fmx_kernels.hpp"
 
@@ -437,6 +440,24 @@ static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup &grp, boo
     return bits;
 }
 
+// k_locate's hand-off tag for one launch: a process-wide launch counter
+// through a bijective mix (odd multiplier, splitmix64 finaliser) with a random
+// nonce — distinct for every launch of this process, and unrelated to the
+// words another process (or nothing) left in a workspace.
+static uint64_t launch_tag() {
+    static const uint64_t nonce = [] {
+        std::random_device rd;
+        return ((uint64_t)rd() << 32) ^ (uint64_t)rd() ^
+               (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    }();
+    static std::atomic<uint64_t> seq{0};
+    uint64_t z = nonce + 0x9E3779B97F4A7C15ull * (seq.fetch_add(1, std::memory_order_relaxed) + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z ? z : 1;  // (0: what zeroed memory holds)
+}
+
 // The kernels of a (grouped) locate, one after another on `stream`.
 static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
                                uint32_t sb, hipStream_t stream, hipEvent_t mid = nullptr) {
@@ -454,8 +475,27 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
     const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= (raw ? ix->grouped_raw_min : ix->grouped_min) &&
                          !grp.tile_ctr &&
                          search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
-    hipError_t e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, stream)
-                           : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
+    // in launch order, batches of at most kFoldTiles tiles of short fixed-length patterns: one kernel
+    // (k_locate), unless the stream is being captured (a replayed graph would reuse the launch's tag)
+    bool fused = !grouped && ix->fused && !grp.tile_ctr && tiles <= ix->fused_max_tiles;
+    for (uint32_t j = 0; fused && j < grp.n; ++j)
+        fused = (grp.b[j].npat + 255) / 256 <= kFoldTiles && grp.b[j].stride != 0 && grp.b[j].stride <= kFusedMaxLen;
+    if (fused) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        fused = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+    }
+    hipError_t e;
+    if (fused) {
+        if ((e = d.ops->locate(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, launch_tag(),
+                               ix->fused_late_ticks, stream)) != hipSuccess)
+            return e;
+        ix->launches_ordered.fetch_add(1, std::memory_order_relaxed);
+        ix->launches_fused.fetch_add(1, std::memory_order_relaxed);
+        // (timing: the whole launch is the first phase)
+        return mid ? hipEventRecord(mid, stream) : hipSuccess;
+    }
+    e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, stream)
+                : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
     (grouped ? (raw ? ix->launches_grouped_raw : ix->launches_grouped) : ix->launches_ordered)
         .fetch_add(1, std::memory_order_relaxed);

@@ -54,7 +54,8 @@ enum hipMemcpyKind {
     hipMemcpyDeviceToDevice = 3,
     hipMemcpyDefault = 4
 };
-enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 63 };
+enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 63, hipDeviceAttributeWallClockRate = 90 };
+enum hipStreamCaptureStatus { hipStreamCaptureStatusNone = 0, hipStreamCaptureStatusActive = 1 };
 typedef struct simt_stream *hipStream_t;
 typedef struct simt_event *hipEvent_t;
 #define hipStreamNonBlocking 1u
@@ -77,6 +78,7 @@ void maybe_yield();  // an atomic's switch point
 // 64 slots (dead / absent lanes hold random bits) and the live-lane mask
 void wave_exchange(uint64_t bits, uint64_t *out, uint64_t *live);
 uint32_t lane_id();
+uint64_t wall_ticks();  // 100 MHz, as the GPU's wall clock
 
 template <class T>
 inline uint64_t to_bits(T v) {
@@ -173,6 +175,25 @@ inline uint64_t atomicAdd(uint64_t *p, uint64_t v) { return ::simt::atomic_add(p
 inline int atomicAdd(int *p, int v) { return ::simt::atomic_add(p, v); }
 inline uint32_t atomicOr(uint32_t *p, uint32_t v) { return ::simt::atomic_or(p, v); }
 
+// k_locate's hand-off (fmx_kernels.hpp, FMX_HANDOFF): plain accesses, each a
+// possible switch point; the wall clock in 10 ns ticks.  Workgroups run one at
+// a time, so a workgroup that waits for another still to run waits out its
+// bound (simt_block_order(1): workgroups in index order, as the GPU
+// dispatches them).
+#define FMX_HANDOFF 1
+inline uint64_t ld_agent(const uint64_t *p) {
+    ::simt::maybe_yield();
+    return __atomic_load_n(p, __ATOMIC_RELAXED);
+}
+inline void st_agent(uint64_t *p, uint64_t v) {
+    __atomic_store_n(p, v, __ATOMIC_RELAXED);
+    ::simt::maybe_yield();
+}
+inline void drain_stores() {}
+inline void poll_pause() { ::simt::maybe_yield(); }
+inline void after_poll() {}
+inline uint64_t wall_ticks() { return ::simt::wall_ticks(); }
+
 // ---------------------------------------------------------------- host API
 hipError_t hipGetLastError();
 const char *hipGetErrorString(hipError_t e);
@@ -195,6 +216,10 @@ hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned flags);
 hipError_t hipStreamCreate(hipStream_t *s);
 hipError_t hipStreamDestroy(hipStream_t s);
 hipError_t hipStreamSynchronize(hipStream_t s);
+inline hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus *st) {
+    *st = hipStreamCaptureStatusNone;
+    return hipSuccess;
+}
 hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned flags = 0);
 hipError_t hipEventCreate(hipEvent_t *e);
 hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned flags);

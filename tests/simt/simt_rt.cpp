@@ -43,6 +43,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <deque>
 #include <cstdlib>
@@ -130,6 +131,7 @@ std::recursive_mutex g_mu;          // one grid at a time
 std::mutex g_rng_mu;                // host-side random fills
 std::mt19937_64 g_rng(0x5eed);
 double g_yield = 0.5;
+bool g_ordered = false;  // workgroups in index order (simt_block_order)
 bool g_inited = false;
 std::vector<Fiber> g_fibers;
 std::vector<Wave> g_waves;
@@ -255,6 +257,11 @@ const dim3 &block_dim() { return g_block; }
 uint8_t *dyn_lds() { return g_dyn.data(); }
 uint32_t lane_id() { return g_cur->lane; }
 
+uint64_t wall_ticks() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count() / 10;
+}
+
 void syncthreads() {
     Fiber &f = *g_cur;
     ++f.nbar;
@@ -314,10 +321,10 @@ hipError_t run_grid(dim3 grid, dim3 block, size_t dyn_bytes, const std::function
     g_body = &body;
     g_tids.resize(nt);
     for (uint32_t t = 0; t < nt; ++t) g_tids[t] = dim3(t % block.x, (t / block.x) % block.y, t / (block.x * block.y));
-    // blocks in a random order
+    // blocks in a random order (simt_block_order(1): in index order)
     std::vector<uint64_t> order(nb);
     for (uint64_t i = 0; i < nb; ++i) order[i] = i;
-    std::shuffle(order.begin(), order.end(), g_rng);
+    if (!g_ordered) std::shuffle(order.begin(), order.end(), g_rng);
     const uint32_t nwaves = (uint32_t)((nt + 63) / 64);
     g_fail.clear();
     for (uint64_t bi : order) {
@@ -411,6 +418,12 @@ void simt_memset_fault(uint64_t size, const uint32_t *words, uint64_t n_words) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     g_memset_fault.assign(words, words + n_words);
     g_memset_fault_size = size;
+}
+// TEST hook: workgroups in index order (1), as the GPU dispatches them, or
+// shuffled (0, the default).
+void simt_block_order(int ordered) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    g_ordered = ordered != 0;
 }
 void simt_stats(uint64_t *grids, uint64_t *items, uint64_t *switches) {
     *grids = g_grids;
@@ -742,7 +755,7 @@ hipError_t hipMemGetInfo(size_t *f, size_t *t) {
     *t = 32ull << 30;
     return hipSuccess;
 }
-hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t, int) {
-    *v = 256;
+hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t a, int) {
+    *v = a == hipDeviceAttributeWallClockRate ? 100000 : 256;  // (kHz)
     return hipSuccess;
 }

@@ -49,14 +49,25 @@ def simt(pkg):
     L.simt_defer.restype = None
     L.simt_selftest_defer.argtypes = []
     L.simt_selftest_defer.restype = C.c_int
+    L.simt_block_order.argtypes = [C.c_int]
+    L.simt_block_order.restype = None
     # deferred streams for every test here: work queued on a stream runs at a
     # random later host call or when the host synchronises, copies read and
     # write host memory when they run (simt_rt.cpp)
     L.simt_defer(1, 0.25)
+    # workgroups run one at a time in a shuffled order here, so the fused
+    # launch (k_locate: a workgroup waits for its batch's earlier tiles) is off
+    # by default and tested with index-ordered workgroups (fused fixture)
+    saved_fused = os.environ.get("FMX_FUSED")
+    os.environ["FMX_FUSED"] = "0"
     saved = n._lib
     n._lib = L
     yield L
     n._lib = saved
+    if saved_fused is None:
+        os.environ.pop("FMX_FUSED", None)
+    else:
+        os.environ["FMX_FUSED"] = saved_fused
 
 
 def pos_of(pkg, pb):
@@ -482,3 +493,133 @@ def test_grouping_policy_simt(pkg, O, simt, monkeypatch):
     assert policy() == (6, 1)
     monkeypatch.setenv("FMX_GROUPED", "0")
     assert policy() == (6, 2 ** 64 - 1)
+
+
+@pytest.fixture
+def fused(simt, monkeypatch):
+    """The fused launch (k_locate) on, workgroups in index order — the order
+    the GPU dispatches them in, which k_locate's waits rely on."""
+    monkeypatch.setenv("FMX_FUSED", "1")
+    simt.simt_block_order(1)
+    yield simt
+    simt.simt_block_order(0)
+
+
+def fused_case(O, rng, pb, planes, vb, sigma, n_text):
+    chars = rand_chr_list(rng, sigma)
+    table = table_from_symbols([bytes([c]) for c in chars])
+    text = rand_text(rng, chars, n_text, n_text)
+    blob = O.build(text, len(chars) + 1, O.layout(pb, planes, vb), 2, 2, table)
+    return chars, text, blob
+
+
+@pytest.mark.parametrize("pb,planes,vb,occ", [(4, 3, 64, 1), (4, 2, 32, 0), (8, 3, 128, 1), (4, 5, 64, 1)])
+def test_fused_locate_simt(pkg, O, fused, pb, planes, vb, occ):
+    """k_locate (search, tile counts handed from workgroup to workgroup,
+    offsets and locations in one kernel) against the oracle: fixed-length
+    batches of five tiles, short patterns (counts of 0, 1 and hundreds: the
+    settled and the dealt emission), long ones (one row each: the row walked
+    during the search), forward and reversed; every launch took the fused
+    path (fmx_index_info.launches_fused)."""
+    fused.simt_config(pb * 1000 + planes * 100 + vb + occ, 0.5)
+    rng = np.random.default_rng(pb * 31 + planes * 7 + vb)
+    chars, text, blob = fused_case(O, rng, pb, planes, vb, min(1 << planes, 12) - 1, 4000)
+    orc = O.OracleIndex(blob, O.layout(pb, planes, vb, 0))
+    ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=occ)
+    launches = 0
+    for m in (3, 17):
+        pats = [rand_pattern(rng, text, m, m) for _ in range(1150)]
+        pats = [p for p in pats if len(p) == m]
+        pats += [bytes(rng.choice(np.frombuffer(chars, np.uint8), size=m)) for _ in range(40)]
+        pats += [chars[:1] * m, chars[-1:] * m]
+        data, offsets = pkg.pack_patterns(pats)
+        ooff, olocs = orc.locate_batch(data, offsets)
+        goff, glocs = ix.locate_batch((data, offsets))
+        assert np.array_equal(goff, ooff), f"m={m}: offsets"
+        assert np.array_equal(glocs, olocs), f"m={m}: locations"
+        roff, rlocs = ix.locate_batch([p[::-1] for p in pats], reversed=True)
+        assert np.array_equal(roff, ooff) and np.array_equal(rlocs, olocs), f"m={m}: reversed"
+        launches += 2
+        assert int(np.diff(ooff).max()) > (1 if m == 3 else 0)
+    info = ix.info()
+    assert info["launches_fused"] == info["launches_ordered"] >= launches, info
+    ix.close()
+
+
+def test_fused_group_garbage_workspaces_simt(pkg, O, fused, monkeypatch):
+    """A fused group launch (fmx_locate_group_async in launch order): 24
+    fixed-length batches of 1-5 tiles, lengths 2..23, every third reversed,
+    workspaces (where the tile counts and their tags live) and outputs full of
+    random bytes, run three times on the same workspaces — a tag left by an
+    earlier launch must never pass for this one's."""
+    monkeypatch.setenv("FMX_GROUPED", "0")
+    fused.simt_config(4242, 0.5)
+    rng = np.random.default_rng(35)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20_000).astype(np.uint8)
+    blob = O.build(text.tobytes(), 5, O.layout(4, 3, 64), 3, 2, table)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    sizes = [int(x) for x in np.random.default_rng(7).integers(1, 1200, size=24)]
+    bats, jobs = [], []
+    for bi, n in enumerate(sizes):
+        rev, m = bi % 3 == 2, 2 + (bi * 5) % 22
+        starts = rng.integers(0, text.size - m, size=n)
+        pats = [text[s:s + m].tobytes() for s in starts]
+        data, offsets = pkg.pack_patterns(pats)
+        want = orc.locate_batch(data, offsets)
+        q = [p[::-1] for p in pats] if rev else pats
+        data, offsets = pkg.pack_patterns(q)
+        cap = int(want[1].size) + 8
+        ws = ix.locate_workspace_size(n)
+        b = dict(n=n, want=want, data=np.concatenate([data, np.zeros(16, np.uint8)]),
+                 off=offsets.view(np.int64).copy(), loff=rng.integers(0, 2**62, size=n + 1).astype(np.int64),
+                 locs=rng.integers(0, 2**31, size=cap).astype(np.int32), need=np.zeros(1, np.int64),
+                 cnt=rng.integers(0, 2**31, size=n).astype(np.int32),
+                 ws=rng.integers(0, 256, size=ws).astype(np.uint8))
+        jobs.append(ix.locate_job(b["data"].ctypes.data, b["off"].ctypes.data, n, b["loff"].ctypes.data,
+                                  b["locs"].ctypes.data, cap, b["need"].ctypes.data, b["ws"].ctypes.data, ws,
+                                  d_counts=b["cnt"].ctypes.data, reversed=rev, stage_kb=max(1, -(-256 * m // 1024)),
+                                  fixed_len=m))
+        bats.append(b)
+    q = ix.job_queue(jobs)
+    for rep in range(3):
+        ix.locate_group_async(q)
+        ix.sync()
+        for b in bats:
+            wo, wl = b["want"]
+            assert np.array_equal(b["loff"].view(np.uint64), wo), f"rep {rep}: offsets"
+            assert np.array_equal(b["locs"][:wl.size].view(np.uint32), wl), f"rep {rep}: locations"
+            assert int(b["need"][0]) == wl.size
+            assert np.array_equal(b["cnt"].view(np.uint32), np.diff(wo).astype(np.uint32))
+    info = ix.info()
+    assert info["launches_fused"] == info["launches_ordered"] == 3, info
+    ix.close()
+
+
+def test_fused_wait_is_bounded_simt(pkg, O, simt, monkeypatch):
+    """k_locate's waits end: with workgroups run in a shuffled order (a later
+    tile before an earlier one, which the GPU's in-order dispatch never does)
+    the waiting workgroups give up after FMX_FUSED_TIMEOUT_MS and the launch
+    reports FMX_E_DEVICE instead of hanging; the next launch, dispatched in
+    order, answers correctly."""
+    monkeypatch.setenv("FMX_FUSED", "1")
+    monkeypatch.setenv("FMX_FUSED_TIMEOUT_MS", "20")
+    simt.simt_config(99, 0.5)
+    rng = np.random.default_rng(3)
+    chars, text, blob = fused_case(O, rng, 4, 3, 64, 4, 3000)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    pats = [text[s:s + 9] for s in rng.integers(0, len(text) - 9, size=8 * 256)]
+    data, offsets = pkg.pack_patterns(pats)
+    with pytest.raises(pkg.FmxError) as ei:
+        ix.locate_batch((data, offsets))
+    assert ei.value.code == pkg._native.FMX_E_DEVICE
+    simt.simt_block_order(1)
+    try:
+        goff, glocs = ix.locate_batch((data, offsets))
+    finally:
+        simt.simt_block_order(0)
+    ooff, olocs = orc.locate_batch(data, offsets)
+    assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    ix.close()
