@@ -753,7 +753,10 @@ def main():
     alg_per_pattern = per_pattern + per_occ * my_occ / max(my_pats, 1)
     per_gpu = value_compute / max(world, 1)
     achieved = alg_per_pattern * per_gpu / 1e9
+    fused0 = ix.info().get("launches_fused", 0)
     kt = kernel_pass(torch, w, max(1, args.kernel_launches))
+    # launches in launch order of small batches run as one kernel (k_locate): its "search phase" is the whole launch
+    fused = ix.info().get("launches_fused", 0) > fused0
     ks, ke, kl = (kt.get(x, {}) for x in ("locate.search", "locate.emit", "locate"))
     ppl = ks.get("units", 0) / max(ks.get("launches", 1), 1)
     search_us = ks["total_ms"] / ks["launches"] * 1e3 if ks.get("launches") else float("nan")
@@ -775,7 +778,9 @@ def main():
         "alg_bytes_per_pattern": alg_per_pattern,
         "kernel": {
             "name": ("search phase of a grouped launch: k_group_key + k_group_scan + k_group_place + "
-                     "k_search_grouped + k_group_tiles" if grouped else "k_search"),
+                     "k_search_grouped + k_group_tiles" if grouped else
+                     "k_locate (fused: search, tile-count hand-off, offsets and locations in one kernel)" if fused
+                     else "k_search"),
             "avg_us": search_us, "patterns_per_launch": ppl,
             "achieved": k_achieved, "frac": k_achieved / HBM_PEAK_GBS,
             "emit_avg_us": ke["total_ms"] / ke["launches"] * 1e3 if ke.get("launches") else None,
