@@ -148,6 +148,8 @@ typedef struct fmx_index_info {
     uint64_t launches_ordered;      /* in launch order,                               */
     uint64_t launches_fused;        /* of those, as one kernel (k_locate: search,
                                        offsets and locations; FMX_FUSED=0: never)   */
+    uint64_t launches_chained;      /* grouped launches ended by k_emit_chain (tile
+                                       counts handed from tile to tile in-kernel)    */
 } fmx_index_info;
 
 typedef struct fmx_kernel_timing {

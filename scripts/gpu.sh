@@ -35,6 +35,8 @@
 #   rawab    C2 grouped with packed vs id-only records (FMX_GROUPED_RAW=1), alternating twice
 #   singletrace  rocprofv3 kernel trace of the single-batch leg (one 100k batch per call)
 #   fusedtest  only tests/test_gpu_fused.py (the fused launch, k_locate)
+#   chainab  C2 (grouped) ended by k_emit_chain vs k_group_tiles + k_emit (FMX_EMIT_CHAIN=0), alternating twice
+#   psweep   C2 at 100k / 200k / 400k patterns per batch (256 batches per launch: 25.6 / 51.2 / 102.4 M per launch)
 #   fusedab  the fused launch vs the two-kernel path (FMX_FUSED=0): single batch, C1, C4, alternating twice;
 #            then the single-batch kernel trace of the fused build
 # Every step has its own time limit; the first failing step ends the run.
@@ -182,6 +184,15 @@ for step in "$@"; do
             done ;;
         fusedtest) run pytest_fused 600 python -u -m pytest tests/test_gpu_fused.py -x -v --timeout 300 \
                 --timeout-method thread || exit 1 ;;
+        chainab)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "chain_on_$r" 300 $B || exit 1
+                FMX_EMIT_CHAIN=0 run "chain_off_$r" 300 $B || exit 1
+            done ;;
+        psweep)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for p in 100000 200000 400000; do run "patterns_$p" 300 $B --patterns $p || exit 1; done ;;
         fusedab)
             for r in 1 2; do
                 run "single_fused_$r" 300 python -u bench.py --single-batch-only || exit 1

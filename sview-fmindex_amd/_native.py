@@ -56,7 +56,8 @@ class fmx_index_info(C.Structure):
                 ("occ_record", C.c_uint32), ("group_key_len", C.c_uint32),
                 ("group_key_base", C.c_uint32), ("grouped_min", C.c_uint64),
                 ("launches_grouped", C.c_uint64), ("launches_grouped_raw", C.c_uint64),
-                ("launches_ordered", C.c_uint64), ("launches_fused", C.c_uint64)]
+                ("launches_ordered", C.c_uint64), ("launches_fused", C.c_uint64),
+                ("launches_chained", C.c_uint64)]
 
 
 class fmx_locate_job(C.Structure):

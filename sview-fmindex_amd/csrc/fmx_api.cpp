@@ -573,6 +573,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (const char *e = getenv("FMX_SEARCH_PERSISTENT")) ix->search_persistent = e[0] == '1';
     // the fused launch (k_locate) and the bound on its waits: 4 s of the wall clock by default
     if (const char *e = getenv("FMX_FUSED")) ix->fused = e[0] != '0';
+    if (const char *e = getenv("FMX_EMIT_CHAIN")) ix->emit_chain = e[0] != '0';
     if (const char *e = getenv("FMX_FUSED_MAX_TILES")) ix->fused_max_tiles = strtoull(e, nullptr, 0);
     {
         uint64_t ms = 4000;
@@ -1104,6 +1105,7 @@ fmx_status fmx_info(const fmx_index *ix, fmx_index_info *o) {
     o->launches_grouped_raw = ix->launches_grouped_raw.load();
     o->launches_ordered = ix->launches_ordered.load();
     o->launches_fused = ix->launches_fused.load();
+    o->launches_chained = ix->launches_chained.load();
     o->device = ix->device;
     return FMX_OK;
 }

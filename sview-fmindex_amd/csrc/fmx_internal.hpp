@@ -241,6 +241,10 @@ struct fmx_index {
     uint64_t fused_max_tiles = ~0ull;
     uint64_t fused_late_ticks = 0;
     mutable std::atomic<uint64_t> launches_fused{0};  // (a subset of launches_ordered)
+    // grouped launches end with k_emit_chain (tile counts handed from tile to tile, as k_locate) instead of
+    // k_group_tiles + k_emit when every batch has at most kFoldTiles tiles (FMX_EMIT_CHAIN=0: never)
+    bool emit_chain = true;
+    mutable std::atomic<uint64_t> launches_chained{0};  // (a subset of the grouped launches)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
     uint64_t dlut_bytes = 0;
@@ -414,6 +418,9 @@ struct LayoutOps {
     // launch order as one kernel (k_locate): tag = the launch's hand-off tag, late_ticks its wait bound
     hipError_t (*locate)(const QueryArgs &qa, uint32_t vb, uint32_t rec, int var, const LocateGroup &grp,
                          uint32_t tiles, uint32_t sb, uint64_t tag, uint64_t late_ticks, hipStream_t s);
+    // a grouped launch's last kernel with the tile counts handed from tile to tile (k_emit_chain)
+    hipError_t (*emit_chain)(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp, uint32_t tiles,
+                             uint64_t tag, uint64_t late_ticks, hipStream_t s);
 };
 uint64_t locate_tiles_cap(uint64_t n);
 // Bytes per pattern of the search-result records in the locate workspace.

@@ -461,6 +461,44 @@ __device__ __forceinline__ void after_poll() { __builtin_amdgcn_fence(__ATOMIC_A
 __device__ __forceinline__ uint64_t wall_ticks() { return wall_clock64(); }
 #endif
 
+// Tile g's base offset in its batch (of G tiles) from the hand-off: publish
+// this tile's count agg (the last tile's is read by no one), then sum the
+// earlier tiles' counts as they are published, lane t taking tiles t, t + 256,
+// ... below g.  Ends with a barrier (s_part).
+__device__ __forceinline__ uint64_t chain_base(const LocateBatch &B, uint64_t G, uint32_t g, uint64_t agg,
+                                               uint64_t tag, uint64_t late_ticks, uint32_t *status,
+                                               uint64_t *s_part /*[4]*/) {
+    uint64_t *cnts = B.tiles, *tags = B.tiles + G;
+    if (threadIdx.x == 0 && g + 1 < G) {
+        st_agent(cnts + g, agg);
+        drain_stores();
+        st_agent(tags + g, tag);
+    }
+    uint64_t part = 0;
+    uint32_t late = 0;
+    if (g) {
+        const uint64_t t_end = wall_ticks() + late_ticks;
+        for (uint64_t t = threadIdx.x; t < g; t += 256) {
+            while (ld_agent(tags + t) != tag) {
+                if (wall_ticks() > t_end) {
+                    late = 1;
+                    break;
+                }
+                poll_pause();
+            }
+            after_poll();
+            part += ld_agent(cnts + t);
+        }
+    }
+    if (late) atomicOr(status, kStatusLate);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) part += __shfl_xor(part, d);
+    if (lane == 0) s_part[wv] = part;
+    __syncthreads();
+    return s_part[0] + s_part[1] + s_part[2] + s_part[3];
+}
+
 template <typename P, int N, int VB, int REC, int VAR>
 __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_locate(const QueryArgs a, const LocateGroup grp,
                                                                                uint32_t stage_bytes, uint64_t tag,
@@ -479,37 +517,7 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_locate(
     const uint64_t cnt = search_lane<P, N, VB, REC, VAR>(a, B, g, s, s_pat, stage_bytes, lo, rloc, mask, mode);
     uint64_t agg;
     const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);  // (its barriers end every read of s_pat)
-    uint64_t *cnts = B.tiles, *tags = B.tiles + G;
-    // publish (the last tile's count is read by no one)
-    if (threadIdx.x == 0 && g + 1 < G) {
-        st_agent(cnts + g, agg);
-        drain_stores();
-        st_agent(tags + g, tag);
-    }
-    // the earlier tiles' counts: lane t takes tiles t, t + 256, ... below g
-    uint64_t part = 0;
-    uint32_t late = 0;
-    if (g) {
-        const uint64_t t_end = wall_ticks() + late_ticks;
-        for (uint64_t t = threadIdx.x; t < g; t += 256) {
-            while (ld_agent(tags + t) != tag) {
-                if (wall_ticks() > t_end) {
-                    late = 1;
-                    break;
-                }
-                poll_pause();
-            }
-            after_poll();
-            part += ld_agent(cnts + t);
-        }
-    }
-    if (late) atomicOr(a.status, kStatusLate);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) part += __shfl_xor(part, d);
-    if (lane == 0) s_part[wv] = part;
-    __syncthreads();
-    const uint64_t base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    const uint64_t base = chain_base(B, G, g, agg, tag, late_ticks, a.status, s_part);
     const uint64_t my_off = base + excl, i = (uint64_t)g * 256u + threadIdx.x;
     if (g + 1 == G && threadIdx.x == 0) {
         B.loc_off[npat] = base + agg;
@@ -1173,6 +1181,42 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
                                       reinterpret_cast<P *>(B.out_locs));
         base = tb + agg;
     }
+}
+
+// A grouped launch's last kernel (replaces k_group_tiles + k_emit): one tile
+// per workgroup reads its patterns' NarrowRec results (written at each
+// pattern's index by k_search_grouped), writes the optional counts, hands its
+// tile's count to the batch's later tiles as k_locate does (chain_base) and
+// writes the offsets and locations.  Its workgroups are short and alike, so
+// the waits are, too.
+template <typename P, int N, int VB, int REC>
+__global__ __launch_bounds__(256) void k_emit_chain(const QueryArgs a, const LocateGroup grp, uint64_t tag,
+                                                    uint64_t late_ticks) {
+    __shared__ P sC[kMaxSigma + 1];
+    __shared__ uint64_t s_scan[4], s_part[4];
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.tab->C[threadIdx.x];
+    const uint32_t jb = group_batch(grp, blockIdx.x);
+    const LocateBatch &B = grp.b[jb];
+    const uint64_t npat = B.npat, G = (npat + 255) / 256;
+    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
+    const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
+    P lo = 0, rloc = 0;
+    uint64_t mask = 0, cnt = 0;
+    uint32_t mode = kHitOne;
+    if (i < npat) {
+        cnt = unpack_narrow<P>(reinterpret_cast<const NarrowRec<P> *>(B.tiles + 2 * G)[i], lo, rloc, mask, mode);
+        if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = (P)cnt;
+    }
+    uint64_t agg;
+    const uint64_t excl = block_excl_scan(cnt, &agg, s_scan);  // (its barriers publish sC)
+    const uint64_t base = chain_base(B, G, g, agg, tag, late_ticks, a.status, s_part);
+    const uint64_t my_off = base + excl;
+    if (g + 1 == G && threadIdx.x == 0) {
+        B.loc_off[npat] = base + agg;
+        *B.needed = base + agg;
+    }
+    if (i < npat) B.loc_off[i] = my_off;
+    emit_locations<P, N, VB, REC>(a, sC, my_off, cnt, lo, rloc, mask, mode, B.cap, reinterpret_cast<P *>(B.out_locs));
 }
 
 // Level j -> j+1: child string cS has code digit(c)*S^j + code(S); its

@@ -186,6 +186,14 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
     });
 }
 
+[[maybe_unused]] hipError_t op_emit_chain(const QueryArgs &qa, uint32_t vb, uint32_t rec, const LocateGroup &grp,
+                                          uint32_t tiles, uint64_t tag, uint64_t late_ticks, hipStream_t s) {
+    return disp(vb, rec, [&]<int VB, int R>() {
+        hipLaunchKernelGGL((k_emit_chain<P, N, VB, R>), dim3(tiles), dim3(256), 0, s, qa, grp, tag, late_ticks);
+        return hipGetLastError();
+    });
+}
+
 }  // namespace
 
 #if !defined(__HIP_DEVICE_COMPILE__)  // a host table (the device pass only instantiates the kernels)
@@ -193,7 +201,8 @@ hipError_t disp(uint32_t vb, uint32_t rec, F &&f) {
 #define FMX_OPS_NAME(p, n, v) FMX_OPS_NAME2(p, n, v)
 extern const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB);
 const LayoutOps FMX_OPS_NAME(FMX_LAYOUT_P, FMX_LAYOUT_N, FMX_LAYOUT_VB) = {op_count, op_search, op_emit, op_search_grouped,
-                                                           op_dlut_level, op_full_sa, op_relayout, op_locate};
+                                                           op_dlut_level, op_full_sa, op_relayout, op_locate,
+                                                           op_emit_chain};
 #endif
 
 }  // namespace fmx

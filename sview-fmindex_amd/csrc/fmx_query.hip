@@ -344,7 +344,8 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
 // A grouped launch's search (kWsHeader): key counts, their scan, the sorted
 // order, the search in key order, tile counts.
 static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t ewg,
-                                        uint64_t total, uint32_t sb, uint32_t bits, bool raw, hipStream_t stream) {
+                                        uint64_t total, uint32_t sb, uint32_t bits, bool raw, bool chain,
+                                        hipStream_t stream) {
     const uint32_t tiles = grp.tile_begin[grp.n - 1] + (uint32_t)((grp.b[grp.n - 1].npat + 255) / 256);
     const Disp d = dispatch(ix);
     grp.gcount = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader + 256);
@@ -418,6 +419,7 @@ static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa
                                    stream)) !=
         hipSuccess)
         return e;
+    if (chain) return hipSuccess;  // (k_emit_chain sums the tiles itself)
     if (p4)
         hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(ewg), dim3(256), 0, stream, grp);
     else
@@ -476,13 +478,16 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
                          !grp.tile_ctr &&
                          search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
     // in launch order, batches of at most kFoldTiles tiles of short fixed-length patterns: one kernel
-    // (k_locate), unless the stream is being captured (a replayed graph would reuse the launch's tag)
-    bool fused = !grouped && ix->fused && !grp.tile_ctr && tiles <= ix->fused_max_tiles;
-    for (uint32_t j = 0; fused && j < grp.n; ++j)
-        fused = (grp.b[j].npat + 255) / 256 <= kFoldTiles && grp.b[j].stride != 0 && grp.b[j].stride <= kFusedMaxLen;
-    if (fused) {
+    // (k_locate); grouped, batches of at most kFoldTiles tiles: k_emit_chain ends the launch — both
+    // unless the stream is being captured (a replayed graph would reuse the launch's tag)
+    bool small = true;
+    for (uint32_t j = 0; small && j < grp.n; ++j) small = (grp.b[j].npat + 255) / 256 <= kFoldTiles;
+    bool fused = !grouped && small && ix->fused && !grp.tile_ctr && tiles <= ix->fused_max_tiles;
+    for (uint32_t j = 0; fused && j < grp.n; ++j) fused = grp.b[j].stride != 0 && grp.b[j].stride <= kFusedMaxLen;
+    bool chain = grouped && small && ix->emit_chain;
+    if (fused || chain) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        fused = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) fused = chain = false;
     }
     hipError_t e;
     if (fused) {
@@ -494,12 +499,16 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
         // (timing: the whole launch is the first phase)
         return mid ? hipEventRecord(mid, stream) : hipSuccess;
     }
-    e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, stream)
+    e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, chain, stream)
                 : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
     if (e != hipSuccess) return e;
     (grouped ? (raw ? ix->launches_grouped_raw : ix->launches_grouped) : ix->launches_ordered)
         .fetch_add(1, std::memory_order_relaxed);
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
+    if (chain) {
+        ix->launches_chained.fetch_add(1, std::memory_order_relaxed);
+        return d.ops->emit_chain(qa, d.vb, d.rec, grp, tiles, launch_tag(), ix->fused_late_ticks, stream);
+    }
     uint32_t fold = 1;
     for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
     if (!fold) {

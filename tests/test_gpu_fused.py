@@ -10,7 +10,9 @@ batches of at most kFoldTiles tiles take it by default (FMX_FUSED=0: never).
   * under uneven load (cdna_hip_programming.md Guideline 16, Pitfall 3): the
     fused launches run on one stream while another stream runs a heavy
     two-kernel launch on the same GPU — every fused result against the oracle;
-  * group launches of 1-8-tile batches on workspaces full of random bytes.
+  * group launches of 1-8-tile batches on workspaces full of random bytes;
+  * grouped launches ended by k_emit_chain (the same hand-off after the
+    grouped search) and by k_group_tiles + k_emit.
 The path each launch took is asserted through fmx_index_info's counters."""
 import numpy as np
 import pytest
@@ -220,4 +222,61 @@ def test_fused_group_launches(pkg, O, monkeypatch):
                 f"rep {rep} batch {bi}: locations"
             assert np.array_equal(b["cnt"].cpu().numpy().view(np.uint32), np.diff(wo).astype(np.uint32))
     assert ix.info()["launches_fused"] - before == 6
+    ix.close()
+
+
+@pytest.mark.parametrize("chain", ["1", "0"])
+def test_chained_grouped_launches(pkg, O, monkeypatch, chain):
+    """Grouped group launches (FMX_GROUPED=1) ended by k_emit_chain (tile
+    counts handed from tile to tile inside the kernel; FMX_EMIT_CHAIN=0: the
+    k_group_tiles + k_emit pair): 300 fixed-length batches of 1-3,000
+    patterns, lengths 1..28, every third reversed, random-byte workspaces and
+    outputs, three rounds: every batch against the oracle, and the launch
+    counters show which ending ran."""
+    import torch
+    rng, text, blob = c2_like(pkg, O, 4_000_000, 54)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_EMIT_CHAIN", chain)
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    dev = torch.device("cuda:0")
+    sizes = [int(x) for x in np.random.default_rng(10).integers(1, 3000, size=300)]
+    bats, jobs = [], []
+    for bi, n in enumerate(sizes):
+        rev, m = bi % 3 == 2, 1 + (bi * 5) % 28
+        starts = rng.integers(0, text.size - m, size=n)
+        pats = [text[s:s + m].tobytes() for s in starts]
+        data, offsets = pkg.pack_patterns(pats)
+        want = orc.locate_batch(data, offsets)
+        q = [p[::-1] for p in pats] if rev else pats
+        data, offsets = pkg.pack_patterns(q)
+        cap = int(want[1].size) + 8
+        ws = ix.locate_workspace_size(n)
+        b = dict(want=want, data=torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).to(dev),
+                 off=torch.from_numpy(offsets.view(np.int64).copy()).to(dev),
+                 loff=torch.randint(0, 2**62, (n + 1,), dtype=torch.int64, device=dev),
+                 locs=torch.randint(0, 2**31 - 1, (cap,), dtype=torch.int32, device=dev),
+                 need=torch.zeros(1, dtype=torch.int64, device=dev),
+                 cnt=torch.randint(0, 2**31 - 1, (n,), dtype=torch.int32, device=dev),
+                 ws=torch.randint(0, 256, (ws,), dtype=torch.uint8, device=dev))
+        jobs.append(ix.locate_job(b["data"].data_ptr(), b["off"].data_ptr(), n, b["loff"].data_ptr(),
+                                  b["locs"].data_ptr(), cap, b["need"].data_ptr(), b["ws"].data_ptr(), ws,
+                                  d_counts=b["cnt"].data_ptr(), reversed=rev, stage_kb=max(1, -(-256 * m // 1024)),
+                                  fixed_len=m))
+        bats.append(b)
+    q = ix.job_queue(jobs)
+    torch.cuda.synchronize()
+    for rep in range(3):
+        ix.locate_group_async(q)
+        ix.sync()
+        for bi, b in enumerate(bats):
+            wo, wl = b["want"]
+            assert np.array_equal(b["loff"].cpu().numpy().view(np.uint64), wo), f"rep {rep} batch {bi}: offsets"
+            assert int(b["need"].item()) == wl.size, f"rep {rep} batch {bi}: total"
+            assert np.array_equal(b["locs"].cpu().numpy()[:wl.size].view(np.uint32), wl), \
+                f"rep {rep} batch {bi}: locations"
+            assert np.array_equal(b["cnt"].cpu().numpy().view(np.uint32), np.diff(wo).astype(np.uint32))
+    info = ix.info()
+    assert info["launches_grouped"] == 6 and info["launches_ordered"] == 0, info
+    assert info["launches_chained"] == (6 if chain == "1" else 0), info
     ix.close()

@@ -58,16 +58,18 @@ def simt(pkg):
     # workgroups run one at a time in a shuffled order here, so the fused
     # launch (k_locate: a workgroup waits for its batch's earlier tiles) is off
     # by default and tested with index-ordered workgroups (fused fixture)
-    saved_fused = os.environ.get("FMX_FUSED")
-    os.environ["FMX_FUSED"] = "0"
+    # (and k_emit_chain, which ends grouped launches the same way)
+    saved_env = {k: os.environ.get(k) for k in ("FMX_FUSED", "FMX_EMIT_CHAIN")}
+    os.environ["FMX_FUSED"] = os.environ["FMX_EMIT_CHAIN"] = "0"
     saved = n._lib
     n._lib = L
     yield L
     n._lib = saved
-    if saved_fused is None:
-        os.environ.pop("FMX_FUSED", None)
-    else:
-        os.environ["FMX_FUSED"] = saved_fused
+    for k, v in saved_env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def pos_of(pkg, pb):
@@ -497,9 +499,11 @@ def test_grouping_policy_simt(pkg, O, simt, monkeypatch):
 
 @pytest.fixture
 def fused(simt, monkeypatch):
-    """The fused launch (k_locate) on, workgroups in index order — the order
-    the GPU dispatches them in, which k_locate's waits rely on."""
+    """The fused launch (k_locate) and the chained grouped emit
+    (k_emit_chain) on, workgroups in index order — the order the GPU
+    dispatches them in, which their waits rely on."""
     monkeypatch.setenv("FMX_FUSED", "1")
+    monkeypatch.setenv("FMX_EMIT_CHAIN", "1")
     simt.simt_block_order(1)
     yield simt
     simt.simt_block_order(0)
@@ -622,4 +626,57 @@ def test_fused_wait_is_bounded_simt(pkg, O, simt, monkeypatch):
         simt.simt_block_order(0)
     ooff, olocs = orc.locate_batch(data, offsets)
     assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    ix.close()
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_chained_grouped_emit_simt(pkg, O, fused, monkeypatch, seed):
+    """Grouped launches ended by k_emit_chain (the tile counts handed from
+    tile to tile inside the kernel) instead of k_group_tiles + k_emit: the
+    group launch of 40 fixed-length batches (1-1,500 patterns, lengths 1..32,
+    every third reversed) on random-byte workspaces, twice, against the
+    oracle; every launch grouped and chained."""
+    monkeypatch.setenv("FMX_GROUPED", "1")
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
+    fused.simt_config(1000 + seed, 0.5)
+    rng = np.random.default_rng(60 + seed)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=30_000).astype(np.uint8)
+    blob = O.build(text.tobytes(), 5, O.layout(4, 3, 64), 3, 2, table)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    sizes = [int(x) for x in np.random.default_rng(6 + seed).integers(1, 1500, size=40)]
+    bats, jobs = [], []
+    for bi, n in enumerate(sizes):
+        rev, m = bi % 3 == 2, 1 + (bi * 7) % 32
+        starts = rng.integers(0, text.size - m, size=n)
+        pats = [text[s:s + m].tobytes() for s in starts]
+        data, offsets = pkg.pack_patterns(pats)
+        want = orc.locate_batch(data, offsets)
+        q = [p[::-1] for p in pats] if rev else pats
+        data, offsets = pkg.pack_patterns(q)
+        cap = int(want[1].size) + 8
+        ws = ix.locate_workspace_size(n)
+        b = dict(n=n, want=want, data=np.concatenate([data, np.zeros(16, np.uint8)]),
+                 off=offsets.view(np.int64).copy(), loff=rng.integers(0, 2**62, size=n + 1).astype(np.int64),
+                 locs=rng.integers(0, 2**31, size=cap).astype(np.int32), need=np.zeros(1, np.int64),
+                 cnt=rng.integers(0, 2**31, size=n).astype(np.int32),
+                 ws=rng.integers(0, 256, size=ws).astype(np.uint8))
+        jobs.append(ix.locate_job(b["data"].ctypes.data, b["off"].ctypes.data, n, b["loff"].ctypes.data,
+                                  b["locs"].ctypes.data, cap, b["need"].ctypes.data, b["ws"].ctypes.data, ws,
+                                  d_counts=b["cnt"].ctypes.data, reversed=rev, stage_kb=max(1, -(-256 * m // 1024)),
+                                  fixed_len=m))
+        bats.append(b)
+    q = ix.job_queue(jobs)
+    for rep in range(2):
+        ix.locate_group_async(q)
+        ix.sync()
+        for b in bats:
+            wo, wl = b["want"]
+            assert np.array_equal(b["loff"].view(np.uint64), wo), f"rep {rep}: offsets"
+            assert np.array_equal(b["locs"][:wl.size].view(np.uint32), wl), f"rep {rep}: locations"
+            assert int(b["need"][0]) == wl.size
+            assert np.array_equal(b["cnt"].view(np.uint32), np.diff(wo).astype(np.uint32))
+    info = ix.info()
+    assert info["launches_grouped"] == info["launches_chained"] == 2, info
     ix.close()
