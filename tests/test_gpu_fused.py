@@ -230,7 +230,7 @@ def test_chained_grouped_launches(pkg, O, monkeypatch, chain):
     """Grouped group launches (FMX_GROUPED=1) ended by k_emit_chain (tile
     counts handed from tile to tile inside the kernel; FMX_EMIT_CHAIN=0: the
     k_group_tiles + k_emit pair): 300 fixed-length batches of 1-3,000
-    patterns, lengths 1..28, every third reversed, random-byte workspaces and
+    patterns, lengths 8..28, every third reversed, random-byte workspaces and
     outputs, three rounds: every batch against the oracle, and the launch
     counters show which ending ran."""
     import torch
@@ -243,7 +243,7 @@ def test_chained_grouped_launches(pkg, O, monkeypatch, chain):
     sizes = [int(x) for x in np.random.default_rng(10).integers(1, 3000, size=300)]
     bats, jobs = [], []
     for bi, n in enumerate(sizes):
-        rev, m = bi % 3 == 2, 1 + (bi * 5) % 28
+        rev, m = bi % 3 == 2, 8 + (bi * 5) % 21  # (from 8: a 4 Mbp text gives a 1-mer ~10^6 locations)
         starts = rng.integers(0, text.size - m, size=n)
         pats = [text[s:s + m].tobytes() for s in starts]
         data, offsets = pkg.pack_patterns(pats)
