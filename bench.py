@@ -152,7 +152,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
     ap.add_argument("--batches", type=int, default=32,
                     help="distinct batches cycled (weak-scaling configs; at least one launch group per stream)")
-    ap.add_argument("--group", type=int, default=None, help="batches per kernel launch (at most 256; default 8; c1: 16; c2, c3: 256)")
+    ap.add_argument("--group", type=int, default=None, help="batches per launch (at most 1024; fmx_locate_group_async; default 8; c1, c2, c3, c4: 256)")
     ap.add_argument("--graph", action="store_true",
                     help="capture one pass (every launch, forked over the streams) in a HIP graph and replay it: "
                          "one host call per pass instead of one per launch (launch-bound configs)")
@@ -538,7 +538,7 @@ def main():
     total = args.total_patterns if args.total_patterns >= 0 else cfg["total"]
     P = cfg["pos"]
     S = max(1, args.streams or cfg.get("streams", 2))
-    GR = max(1, min(args.group or cfg.get("group", 8), 256))
+    GR = max(1, min(args.group or cfg.get("group", 8), 1024))
     BLK = cfg["planes"] * cfg["vec"] // 8
     position = pkg.u32 if P == 4 else pkg.u64
     block = getattr(pkg.blocks, f"Block{cfg['planes']}")(pkg.Vector(cfg["vec"]))

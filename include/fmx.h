@@ -234,8 +234,9 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
                                  uint64_t n_patterns, uint32_t flags, void *d_counts, void *stream);
 
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
- * [256 B][32 KiB of key counters][tile counts][tile offsets][one search
- * record per pattern][to 16 B][one 16-B sorted-order record per pattern].
+ * [256 B][32 KiB of key counters][44 KiB batch table of a grouped launch]
+ * [tile counts][tile offsets][one search record per pattern][to 16 B][one
+ * 16-B sorted-order record per pattern].
  * The workspace must be 16-byte aligned (FMX_E_ARG otherwise: the grouped
  * passes read and write it as 16-B vectors; hipMalloc gives 256-B alignment).
  * A workspace needs no initialisation (a grouped launch zeroes its key
@@ -253,8 +254,13 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
  * records, FMX_GROUP_REFINE_MIN=<patterns> re-sorts each key's run by the
  * next symbols, FMX_GROUPED_WSORT=0 turns off the search's in-workgroup sort
  * by the next symbols, FMX_GROUP_CHECK=1 checks each launch's sorted order on
- * the device before its search — a violation is FMX_E_DEVICE; debug).  No
- * kernel makes one workgroup wait on another. */
+ * the device before its search — a violation is FMX_E_DEVICE; debug).  One
+ * kernel makes workgroups wait on others: the fused launch in launch order
+ * (k_locate, fmx_index_info.launches_fused; FMX_FUSED=0 never) — a workgroup
+ * waits for the lower-indexed workgroups of its batch, which the dispatcher
+ * started before it; bounded (FMX_FUSED_TIMEOUT_MS, default 4 s, then
+ * FMX_E_DEVICE).  The key counters and the batch table of a grouped launch
+ * are in its first batch's workspace. */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)
@@ -287,10 +293,12 @@ typedef struct fmx_locate_job {
 
 fmx_status fmx_locate_jobs_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs);
 
-/* The same batches run together: up to 256 per kernel launch on `stream` (each
+/* The same batches run together: up to 1,024 per launch on `stream` (each
  * batch keeps its own patterns, outputs and workspace; the jobs' own stream
  * fields are ignored), so that small batches fill the GPU the way one large
- * batch does.  The jobs' workspaces must be distinct and no two jobs may share
+ * batch does — a grouped launch searches all of them in one order (kernels
+ * take at most 256 batches as arguments: the launch-order path runs one
+ * launch per 256).  The jobs' workspaces must be distinct and no two jobs may share
  * an output buffer (they run concurrently).  The results are those of
  * fmx_locate_batch_async on each job. */
 fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uint64_t n_jobs, void *stream);

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <thread>
 #include <vector>
@@ -1187,15 +1188,20 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
     }
     DeviceGuard dg(ix->device);
     return with_status(ix, s, [&](uint32_t *status) -> fmx_status {
-    // up to kMaxGroup non-empty batches per launch; empty ones get their
-    // zero offset and total directly
+    // up to kMaxMega non-empty batches per launch, as groups of kMaxGroup (one
+    // grouped launch over all of them, or one launch in launch order per
+    // group: launch_locate_groups); empty ones get their zero offset and total
+    // directly
+    constexpr uint32_t kGroups = kMaxMega / kMaxGroup;
+    std::unique_ptr<LocateGroup[]> grps(new (std::nothrow) LocateGroup[kGroups]);
+    if (!grps) return FMX_E_DEVICE;
     uint64_t i = 0;
     while (i < n_jobs) {
-        LocateGroup grp;  // (the first grp.n entries are filled below; group_reset clears the rest that is read)
-        group_reset(grp);
-        uint32_t stage = 0, tiles = 0;
+        uint32_t ng = 0, stage = 0;
         uint64_t units = 0;
-        for (; i < n_jobs && grp.n < kMaxGroup; ++i) {
+        group_reset(grps[0]);
+        uint32_t tiles = 0;
+        for (; i < n_jobs; ++i) {
             const fmx_locate_job &j = jobs[i];
             if (j.n_patterns == 0) {
                 hipError_t e = hipMemsetAsync(j.d_loc_offsets, 0, 8, s);
@@ -1203,6 +1209,12 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
                 if (e != hipSuccess) return FMX_E_DEVICE;
                 continue;
             }
+            if (grps[ng].n == kMaxGroup) {  // the next group
+                if (ng + 1 == kGroups) break;
+                group_reset(grps[++ng]);
+                tiles = 0;
+            }
+            LocateGroup &grp = grps[ng];
             const uint64_t G = locate_tiles_cap(j.n_patterns);
             grp.tile_begin[grp.n] = tiles;
             grp.b[grp.n++] = LocateBatch{j.d_bytes, j.d_offsets, j.n_patterns, j.d_counts, j.d_loc_offsets,
@@ -1215,14 +1227,16 @@ fmx_status fmx_locate_group_async(fmx_index *ix, const fmx_locate_job *jobs, uin
             if (kb > kbs) stage = (stage & ~0xff00u) | (kb << 8);
             stage |= j.flags & FMX_HINT_LONG_PATTERNS;
         }
-        if (grp.n == 0) continue;
+        if (grps[0].n == 0) continue;
+        const uint32_t ngroups = grps[ng].n ? ng + 1 : ng;
         // (A/B) the persistent grid's tile counter: batch 0's workspace header
-        if (ix->search_persistent && ix->occ_mode == FMX_OCC_INTERLEAVED && !ix->qa.dlut && !ix->qa.safull &&
-            !ix->qa.text)
-            grp.tile_ctr = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader);
+        if (ngroups == 1 && ix->search_persistent && ix->occ_mode == FMX_OCC_INTERLEAVED && !ix->qa.dlut &&
+            !ix->qa.safull && !ix->qa.text)
+            grps[0].tile_ctr =
+                reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grps[0].b[0].tiles) - kWsHeader);
         const fmx_status st = dev_err(timed_split(ix, "locate", "locate.search", "locate.emit", s, units,
                                                   [&](hipEvent_t mid) {
-            return launch_locate_group(ix, grp, stage, status, s, mid);
+            return launch_locate_groups(ix, grps.get(), ngroups, stage, status, s, mid);
         }));
         if (st) return st;
     }

@@ -241,9 +241,10 @@ struct fmx_index {
     uint64_t fused_max_tiles = ~0ull;
     uint64_t fused_late_ticks = 0;
     mutable std::atomic<uint64_t> launches_fused{0};  // (a subset of launches_ordered)
-    // grouped launches end with k_emit_chain (tile counts handed from tile to tile, as k_locate) instead of
-    // k_group_tiles + k_emit when every batch has at most kFoldTiles tiles (FMX_EMIT_CHAIN=0: never)
-    bool emit_chain = true;
+    // FMX_EMIT_CHAIN=1 (A/B): grouped launches end with k_emit_chain (tile counts handed from tile to tile,
+    // as k_locate) instead of k_group_tiles + k_emit, when every batch has at most kFoldTiles tiles
+    // (680 vs 235 us per C2 launch: the polls of ~2,000 short resident workgroups, profiles/r5/r5w_chain_*)
+    bool emit_chain = false;
     mutable std::atomic<uint64_t> launches_chained{0};  // (a subset of the grouped launches)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;
@@ -320,6 +321,13 @@ struct LocateGroup {
     uint32_t graw;  // 1: the sorted records hold pattern ids alone (patterns too long to pack)
     uint64_t gtotal;
     uint32_t chunk_begin[kMaxGroup];
+    // A grouped launch may span several LocateGroups (kernel arguments of at
+    // most kMaxGroup batches): gn batches in all, this group's tiles are the
+    // launch's tiles vbase + tile_begin[j] (pattern ids (vbase + tile_begin[j])
+    // x 256 + i), and gtab (the launch's first batch's workspace) maps a
+    // sorted position or a pattern id of the whole launch to its batch
+    const struct GroupTab *gtab;
+    uint32_t gn, vbase;
     // FMX_SEARCH_PERSISTENT=1 (A/B): k_search runs a resident-sized grid whose
     // workgroups take tiles from this counter (batch 0's workspace header,
     // zero between launches: k_emit resets it); null = one workgroup per tile
@@ -333,12 +341,19 @@ inline void group_reset(LocateGroup &g) {
     g.gcount = nullptr;
     g.gkey_len = g.gkey_base = g.gbits = g.graw = 0;
     g.gtotal = 0;
+    g.gtab = nullptr;
+    g.gn = g.vbase = 0;
     g.tile_ctr = nullptr;
 }
 // `mid` (optional): an event recorded between k_search and k_emit (timing).
 // Fills grp's per-launch fields (first, emit_begin, the grouped fields) in place.
 hipError_t launch_locate_group(const fmx_index *ix, LocateGroup &grp, uint32_t stage_flags,
                                uint32_t *status, hipStream_t stream, hipEvent_t mid = nullptr);
+// Up to kMaxMega batches as ng LocateGroups (each filled as for
+// launch_locate_group, tile_begin[0] = 0 in each): one grouped launch over all
+// of them when the launch is grouped, else each group in launch order.
+hipError_t launch_locate_groups(const fmx_index *ix, LocateGroup *grps, uint32_t ng, uint32_t stage_flags,
+                                uint32_t *status, hipStream_t stream, hipEvent_t mid = nullptr);
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;
@@ -391,7 +406,33 @@ constexpr uint32_t kGroupedXcd = 1;  // k_search_grouped opts: deal the key orde
 constexpr uint32_t kWsortBytes = 1024 + 256 * 16;  // its in-workgroup sort's LDS (256 counters, 256 records)
 constexpr uint32_t kGroupRawStage = 216;  // raw records: patterns up to this long are staged in LDS by the search
 constexpr uint32_t kGroupCounterRoom = kGroupBins;
-constexpr uint64_t kWsHeader = 256 + 4ull * kGroupCounterRoom;
+// Batches per grouped launch: up to kMaxMega, as several LocateGroups of at
+// most kMaxGroup (kernel arguments) whose key, place, tile and emit kernels run
+// per group and whose count scan, refine and search run once over the whole
+// launch (fmx_query.hip, launch_locate_groups).  Each doubling of a grouped
+// launch read fewer lines per pattern: C2's search 271 / 248 / 236 ns per
+// pattern at 25.6 / 51.2 / 102.4 M patterns per launch (profiles/r5/r5w_*).
+#ifndef FMX_MAX_MEGA
+#define FMX_MAX_MEGA 1024
+#endif
+constexpr uint32_t kMaxMega = FMX_MAX_MEGA;
+// A grouped launch's batch table, what its kernels read per lane to find the
+// batch of a sorted position or a pattern id (binary searches; the arrays stay
+// in L1).  In the launch's first batch's workspace, after the key counters;
+// uploaded (pinned stage) before the launch's first kernel.
+struct GroupDesc {
+    uint8_t *recs;          // the batch's search records (a grouped launch: NarrowRec<P>)
+    void *sorted;           // its share of the sorted order (U4 records)
+    const uint8_t *bytes;   // its patterns (id-only records: read by the search)
+    uint32_t stride, rev;
+};
+struct GroupTab {
+    uint64_t first[kMaxMega];   // the launch's sorted positions (= patterns) before batch j
+    uint32_t vfirst[kMaxMega];  // batch j's first pattern id
+    GroupDesc desc[kMaxMega];
+};
+constexpr uint64_t kWsGroupTab = 256 + 4ull * kGroupCounterRoom;  // (16-B aligned)
+constexpr uint64_t kWsHeader = kWsGroupTab + ((sizeof(GroupTab) + 15) & ~15ull);
 inline uint64_t group_chunks(uint64_t n) { return ((n + 255) / 256 + kGroupChunkTiles - 1) / kGroupChunkTiles; }
 
 // The kernels that depend on the occ layout, one table per (P, N) pair

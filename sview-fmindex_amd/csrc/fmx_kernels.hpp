@@ -601,13 +601,7 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     __shared__ uint8_t s_dig[kMaxSigma];
     __shared__ uint32_t s_pw[32];
     __shared__ uint32_t hist[kGroupBins];
-    __shared__ U4 *s_sorted[kMaxGroup];
-    __shared__ uint64_t s_first[kMaxGroup];
     const uint32_t t = threadIdx.x;
-    if (PLACE && t < grp.n) {
-        s_sorted[t] = group_sorted(grp.b[t], rec_bytes);
-        s_first[t] = grp.b[t].first;
-    }
     if (t < 256) s_enc[t] = a.tab->enc[t];
     if (t < (uint32_t)kMaxSigma) s_dig[t] = a.tab->dig[t] == kNoDigit ? 0 : a.tab->dig[t];  // (absent: occurs nowhere)
     if (t == 0) {
@@ -701,7 +695,7 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
             rec_r[p].x = (uint32_t)lo;
             rec_r[p].y = (uint32_t)(lo >> 32);
             rec_r[p].z = (uint32_t)hi;
-            rec_r[p].w = (uint32_t)(grp.tile_begin[jb] * 256ull + i);
+            rec_r[p].w = (uint32_t)((grp.vbase + (uint64_t)grp.tile_begin[jb]) * 256ull + i);
         } else {
             atomicAdd(&hist[key], 1u);
         }
@@ -737,8 +731,10 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
                 atomicOr(a.status, kStatusGroup);
                 continue;
             }
-            const uint32_t js = lds_upper(s_first, grp.n, sp);
-            s_sorted[js][sp - s_first[js]] = rec_r[p];
+            // the batch holding sorted position sp (the launch's batch table, GroupTab)
+            const GroupTab &gt = *grp.gtab;
+            const uint32_t js = lds_upper(gt.first, grp.gn, sp);
+            reinterpret_cast<U4 *>(gt.desc[js].sorted)[sp - gt.first[js]] = rec_r[p];
         }
     }
 }
@@ -777,20 +773,12 @@ template <int UNUSED = 0>
 __global__ __launch_bounds__(1024) void k_group_refine(const QueryArgs a, const LocateGroup grp, uint32_t rec_bytes) {
     constexpr uint32_t T = 1024, per = kGroupBins / T, NW = T / 64;
     __shared__ uint32_t hist[kGroupBins];
-    __shared__ U4 *s_sorted[kMaxGroup];
-    __shared__ uint64_t s_first[kMaxGroup];
-    __shared__ uint32_t s_vfirst[kMaxGroup], s_stride[kMaxGroup];
     __shared__ uint8_t s_dig[kMaxSigma + 1];
     __shared__ uint32_t s_pw[32];
     __shared__ uint32_t s_wsum[NW];
     const uint32_t t = threadIdx.x;
     const uint64_t total = grp.gtotal;
-    if (t < grp.n) {
-        s_sorted[t] = group_sorted(grp.b[t], rec_bytes);
-        s_first[t] = grp.b[t].first;
-        s_vfirst[t] = grp.tile_begin[t] * 256u;
-        s_stride[t] = grp.b[t].stride;
-    }
+    const GroupTab &gt = *grp.gtab;  // (the launch's batches: a sorted position's or a pattern id's batch)
     const uint32_t sym_max = a.sigma, L = grp.gkey_len, bits = grp.gbits;
     if (t <= (uint32_t)kMaxSigma) s_dig[t] = t < sym_max && a.tab->dig[t] != kNoDigit ? a.tab->dig[t] : 0;
     if (t == 0) {
@@ -818,14 +806,14 @@ __global__ __launch_bounds__(1024) void k_group_refine(const QueryArgs a, const 
             const uint64_t p = s0 + u * T + t;
             key[u] = rank[u] = 0;
             if (p >= s0 + sn) continue;
-            const uint32_t js = lds_upper(s_first, grp.n, p);
-            rec[u] = s_sorted[js][p - s_first[js]];
+            const uint32_t js = lds_upper(gt.first, grp.gn, p);
+            rec[u] = reinterpret_cast<const U4 *>(gt.desc[js].sorted)[p - gt.first[js]];
         }
 #pragma unroll
         for (uint32_t u = 0; u < kRefinePer; ++u) {
             const uint64_t p = s0 + u * T + t;
             if (p >= s0 + sn) continue;
-            const uint32_t m = s_stride[lds_upper(s_vfirst, grp.n, rec[u].w)];
+            const uint32_t m = gt.desc[lds_upper(gt.vfirst, grp.gn, rec[u].w)].stride;
             uint32_t k2 = 0;
             for (uint32_t d = 0; d < L; ++d) {
                 const uint32_t back = L + d;  // 0 = the pattern's last symbol
@@ -865,23 +853,14 @@ __global__ __launch_bounds__(1024) void k_group_refine(const QueryArgs a, const 
             const uint64_t p = s0 + u * T + t;
             if (p >= s0 + sn) continue;
             const uint64_t np = s0 + hist[key[u]] + rank[u];
-            const uint32_t js = lds_upper(s_first, grp.n, np);
-            s_sorted[js][np - s_first[js]] = rec[u];
+            const uint32_t js = lds_upper(gt.first, grp.gn, np);
+            reinterpret_cast<U4 *>(gt.desc[js].sorted)[np - gt.first[js]] = rec[u];
         }
         __syncthreads();  // (the next segment's histogram)
     }
     }
 }
 
-// What k_search_grouped needs of each batch, staged in LDS (the batch of a
-// lane's pattern is per lane here, not per workgroup).
-template <typename P>
-struct GroupBatch {
-    SearchRec<P> *recs;
-    const U4 *sorted;
-    const uint8_t *bytes;  // (raw records: the patterns, read by the search)
-    uint32_t stride, rev;
-};
 
 // 3. Search the launch's patterns in key order: workgroup b takes sorted
 // positions [256 K b, 256 K (b + 1)), K = 1 or 2 patterns per lane (lane t:
@@ -929,9 +908,6 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
                                                            uint64_t total, uint32_t cap, uint32_t opts) {
     static_assert(K == 1 || K == 2, "one or two patterns per lane");
     __shared__ Tables<P> s;
-    __shared__ GroupBatch<P> sb[kMaxGroup];
-    __shared__ uint64_t s_first[kMaxGroup];   // the launch's patterns before batch j
-    __shared__ uint32_t s_vfirst[kMaxGroup];  // batch j's first pattern id (tile_begin * 256)
     __shared__ uint8_t s_dig[kMaxSigma + 1];  // (wsort) symbol -> digit; sigma (past the pattern's start) -> 0
     __shared__ uint64_t s_wscan[4];
     const uint32_t wsort = K == 1 && !grp.graw ? (opts >> 8) & 0xffu : 0u, xcd = opts & kGroupedXcd;
@@ -941,17 +917,8 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     if (threadIdx.x <= (uint32_t)kMaxSigma)
         s_dig[threadIdx.x] =
             threadIdx.x < a.sigma && a.tab->dig[threadIdx.x] != kNoDigit ? a.tab->dig[threadIdx.x] : 0;
-    for (uint32_t j = threadIdx.x; j < grp.n; j += 256) {
-        const LocateBatch &B = grp.b[j];
-        const uint64_t G = (B.npat + 255) / 256;
-        sb[j].recs = reinterpret_cast<SearchRec<P> *>(B.tiles + 2 * G);
-        sb[j].sorted = group_sorted(B, sizeof(SearchRec<P>));
-        sb[j].bytes = B.bytes;
-        sb[j].stride = B.stride;
-        sb[j].rev = B.rev;
-        s_first[j] = B.first;
-        s_vfirst[j] = grp.tile_begin[j] * 256u;
-    }
+    // (the launch's batches, GroupTab: each lane finds its pattern's batch by binary searches there)
+    const GroupTab &gt = *grp.gtab;
     __syncthreads();
     // xcd: workgroup b takes chunk start(b % 8) + b / 8, so that (under the
     // round-robin placement of workgroups over the 8 XCDs, which only speed
@@ -964,13 +931,13 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     PatView pv[K];
     bool live[K];
     uint64_t pi[K];
-    uint32_t pj[K];
+    uint8_t *recp[K];
 #pragma unroll
     for (int q = 0; q < K; ++q) {
         const uint64_t sp = (uint64_t)chunk * (256u * K) + (uint32_t)q * 256u + threadIdx.x;
         live[q] = sp < total;
         pi[q] = 0;
-        pj[q] = 0;
+        recp[q] = nullptr;
         uint8_t *dst = s_pat + ((uint32_t)q * 256u + threadIdx.x) * cap;
         pv[q].m = 0;
         pv[q].rev = false;
@@ -978,13 +945,13 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         pv[q].enc = s.enc;
         pv[q].sym = dst;
         if (!live[q]) continue;
-        const uint32_t js = lds_upper(s_first, grp.n, sp);
-        U4 e = sb[js].sorted[sp - s_first[js]];
+        const uint32_t js = lds_upper(gt.first, grp.gn, sp);
+        U4 e = reinterpret_cast<const U4 *>(gt.desc[js].sorted)[sp - gt.first[js]];
         if (K == 1 && wsort && (uint64_t)chunk * 256u + 256u <= total) {  // (workgroup-uniform: all lanes live)
             uint32_t *hist = reinterpret_cast<uint32_t *>(s_pat);
             U4 *stage = reinterpret_cast<U4 *>(s_pat + 1024);
             const uint32_t t = threadIdx.x, base = grp.gkey_base;
-            const uint32_t m = sb[lds_upper(s_vfirst, grp.n, e.w)].stride;
+            const uint32_t m = gt.desc[lds_upper(gt.vfirst, grp.gn, e.w)].stride;
             uint32_t k2 = 0;
             for (uint32_t d = 0; d < wsort; ++d) {
                 const uint32_t back = wskip + d;  // 0 = the pattern's last symbol
@@ -1004,20 +971,21 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
             __syncthreads();  // (the stage is s_pat: every lane has its record before any unpacks)
         }
         const uint32_t v = e.w;
-        const uint32_t jb = lds_upper(s_vfirst, grp.n, v);
-        pj[q] = jb;
-        pi[q] = (uint64_t)(v - s_vfirst[jb]);
-        pv[q].m = sb[jb].stride;
+        const uint32_t jb = lds_upper(gt.vfirst, grp.gn, v);
+        const GroupDesc dj = gt.desc[jb];
+        recp[q] = dj.recs;
+        pi[q] = (uint64_t)(v - gt.vfirst[jb]);
+        pv[q].m = dj.stride;
         if (grp.graw) {
-            const uint32_t m = sb[jb].stride;
-            const uint8_t *src = sb[jb].bytes + pi[q] * m;
+            const uint32_t m = dj.stride;
+            const uint8_t *src = dj.bytes + pi[q] * m;
             if (cap >= m) {
                 // the pattern's bytes (input order) into its cap bytes of LDS,
                 // encoded, in pattern order: aligned 16-B vectors, four in
                 // flight per round trip (grp.graw with m <= kGroupRawStage)
                 const uint64_t a = reinterpret_cast<uint64_t>(src), a0 = a & ~15ull;
                 const uint32_t lead = (uint32_t)(a - a0), nv = (lead + m + 15) >> 4;
-                const bool rv = sb[jb].rev != 0;
+                const bool rv = dj.rev != 0;
                 const U4 *vp = reinterpret_cast<const U4 *>(a0);
                 for (uint32_t v0 = 0; v0 < nv; v0 += 4) {
                     U4 x[4];
@@ -1036,11 +1004,11 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
                 }
             } else {  // longer than the LDS room: the bytes from HBM, encoded on each access
                 pv[q].raw = src;
-                pv[q].rev = sb[jb].rev != 0;
+                pv[q].rev = dj.rev != 0;
                 pv[q].sym = nullptr;
             }
         } else {
-            grouped_unpack<P>(e, sb[jb].stride, grp.gbits, dst);
+            grouped_unpack<P>(e, dj.stride, grp.gbits, dst);
         }
     }
     P lo_r[K], hi_r[K], rloc[K];
@@ -1083,7 +1051,7 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
 #pragma unroll
     for (int q = 0; q < K; ++q)
         if (live[q])
-            reinterpret_cast<NarrowRec<P> *>(sb[pj[q]].recs)[pi[q]] =
+            reinterpret_cast<NarrowRec<P> *>(recp[q])[pi[q]] =
                 NarrowRec<P>{mode[q] == kHitOne ? rloc[q] : lo_r[q], (P)(hi_r[q] - lo_r[q])};
 }
 

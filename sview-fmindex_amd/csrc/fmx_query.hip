@@ -25,6 +25,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <random>
 
 #include "fmx_kernels.hpp"
@@ -149,16 +150,11 @@ __global__ __launch_bounds__(256) void k_group_check_tally(const QueryArgs a, co
 // 2. each sorted position (one per thread)
 __global__ __launch_bounds__(256) void k_group_check_order(const QueryArgs a, const LocateGroup grp,
                                                            uint32_t rec_bytes) {
-    __shared__ uint64_t s_first[kMaxGroup];
-    __shared__ uint32_t s_vfirst[kMaxGroup];
     __shared__ uint8_t s_enc[256];
     __shared__ uint8_t s_dig[kMaxSigma];
     __shared__ uint32_t s_pw[32];
     const uint32_t t = threadIdx.x, L = grp.gkey_len;
-    for (uint32_t j = t; j < grp.n; j += 256) {
-        s_first[j] = grp.b[j].first;
-        s_vfirst[j] = grp.tile_begin[j] * 256u;
-    }
+    const GroupTab &gt = *grp.gtab;  // (the launch's batches)
     s_enc[t] = a.tab->enc[t];
     if (t < (uint32_t)kMaxSigma) s_dig[t] = a.tab->dig[t] == kNoDigit ? 0 : a.tab->dig[t];
     if (t == 0) {
@@ -172,16 +168,17 @@ __global__ __launch_bounds__(256) void k_group_check_order(const QueryArgs a, co
     const uint64_t sp = (uint64_t)blockIdx.x * 256u + t, total = grp.gtotal;
     if (sp >= total) return;
     bool bad = grp.gcount[kGroupBins - 1] != total;  // (the last run ends at the launch's end)
-    const uint32_t js = lds_upper(s_first, grp.n, sp);
-    const U4 e = group_sorted(grp.b[js], rec_bytes)[sp - s_first[js]];
-    const uint32_t jb = lds_upper(s_vfirst, grp.n, e.w);
-    const LocateBatch &B = grp.b[jb];
-    const uint64_t i = (uint64_t)(e.w - s_vfirst[jb]);
-    if (e.w < s_vfirst[jb] || i >= B.npat) {
+    const uint32_t js = lds_upper(gt.first, grp.gn, sp);
+    const U4 e = reinterpret_cast<const U4 *>(gt.desc[js].sorted)[sp - gt.first[js]];
+    const uint32_t jb = lds_upper(gt.vfirst, grp.gn, e.w);
+    const GroupDesc B = gt.desc[jb];
+    const uint64_t i = (uint64_t)(e.w - gt.vfirst[jb]);
+    const uint64_t npat = (jb + 1 < grp.gn ? gt.first[jb + 1] : total) - gt.first[jb];
+    if (e.w < gt.vfirst[jb] || i >= npat) {
         atomicOr(a.status, kStatusCheck);
         return;
     }
-    atomicAdd(group_tally(B) + i, 1u);
+    atomicAdd(reinterpret_cast<uint32_t *>(B.recs) + i, 1u);  // (the batch's tallies: group_tally)
     // the run holding sp: the first key whose end is past it
     uint32_t lo = 0, hi = kGroupBins - 1;
     while (lo < hi) {
@@ -341,107 +338,6 @@ hipError_t launch_count(const fmx_index *ix, const uint8_t *d_bytes, const uint6
     return d.ops->count(qa, d.vb, d.rec, search_var(qa, sb), d_bytes, d_offsets, n, flags, d_counts, sb, stream);
 }
 
-// A grouped launch's search (kWsHeader): key counts, their scan, the sorted
-// order, the search in key order, tile counts.
-static hipError_t launch_grouped_search(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t ewg,
-                                        uint64_t total, uint32_t sb, uint32_t bits, bool raw, bool chain,
-                                        hipStream_t stream) {
-    const uint32_t tiles = grp.tile_begin[grp.n - 1] + (uint32_t)((grp.b[grp.n - 1].npat + 255) / 256);
-    const Disp d = dispatch(ix);
-    grp.gcount = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(grp.b[0].tiles) - kWsHeader + 256);
-    grp.gkey_len = ix->gkey_len;
-    grp.gkey_base = ix->gkey_base;
-    grp.gbits = bits;
-    grp.graw = raw ? 1u : 0u;
-    grp.gtotal = total;
-    // the key counters start at zero whatever an earlier launch on this
-    // workspace did: ordered before the count pass on the stream
-    hipError_t e = hipMemsetAsync(grp.gcount, 0, 4ull * kGroupBins, stream);
-    if (e != hipSuccess) return e;
-    uint32_t chunks = 0;
-    for (uint32_t j = 0; j < grp.n; ++j) {
-        grp.chunk_begin[j] = chunks;
-        chunks += (uint32_t)group_chunks(grp.b[j].npat);
-    }
-    const bool p4 = ix->bv.L.pos_bytes == 4;
-    const uint32_t rb = (uint32_t)locate_rec_bytes(ix->bv.L.pos_bytes);
-    // the key passes hold each pattern in W registers
-    uint32_t maxm = 1;
-    for (uint32_t j = 0; j < grp.n; ++j) maxm = std::max<uint32_t>(maxm, grp.b[j].stride);
-    // (W = 6 words hold patterns up to 21 bytes at any alignment, 8 up to 29, 25 up to 97; raw: the key's
-    // gkey_len <= 16 bytes in 5)
-    // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the
-    // id-only variant's count pass, for packed records too: the decode, one LDS lookup per byte, bounds
-    // these passes, not their loads — profiles/r4/r4q_*, r4r_*)
-    hipLaunchKernelGGL((k_group_key<5, false, true>), dim3((chunks + kCountChunks - 1) / kCountChunks), dim3(1024), 0,
-                       stream, qa, grp, rb);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, grp.gcount);
-    if (raw)
-        hipLaunchKernelGGL((k_group_key<5, true, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    else if (maxm <= 21)
-        hipLaunchKernelGGL((k_group_key<6, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    else if (maxm <= 29)
-        hipLaunchKernelGGL((k_group_key<8, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    else
-        hipLaunchKernelGGL((k_group_key<25, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const bool refined = !raw && total >= ix->group_refine_min;
-    if (refined) {
-        // one workgroup per key from 4,096 patterns per key on average (C2's 25.6 M: every key its own)
-        const uint32_t rg = (uint32_t)std::min<uint64_t>(kGroupBins, std::max<uint64_t>(1, total / 4096));
-        hipLaunchKernelGGL(k_group_refine<0>, dim3(rg), dim3(1024), 0, stream, qa, grp, rb);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    if (ix->group_check) {
-        const uint32_t ord = (uint32_t)((total + 255) / 256);
-        hipLaunchKernelGGL(k_group_check_tally<true>, dim3(tiles), dim3(256), 0, stream, qa, grp);
-        hipLaunchKernelGGL(k_group_check_order, dim3(ord), dim3(256), 0, stream, qa, grp, rb);
-        hipLaunchKernelGGL(k_group_check_tally<false>, dim3(tiles), dim3(256), 0, stream, qa, grp);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    // each lane unpacks (or, raw, stages) its pattern into `cap` bytes of LDS: the longest batch's length,
-    // 4-byte aligned (raw records longer than kGroupRawStage: the search reads the bytes from HBM, cap 4)
-    uint32_t cap = 4;
-    for (uint32_t j = 0; j < grp.n; ++j) cap = std::max<uint32_t>(cap, (grp.b[j].stride + 3) & ~3u);
-    if (raw && cap > kGroupRawStage) cap = 4;
-    // (two patterns per lane: packed records only — 512 lanes' staging would not fit LDS)
-    // the in-workgroup sort's symbols: as many after those already in order (the key's, and the refine
-    // pass's as many again) as base^w <= 256 allows (none when every pattern ends within them)
-    const uint32_t sorted_len = grp.gkey_len * (refined ? 2u : 1u);
-    uint32_t wsort = 0;
-    if (ix->grouped_wsort && !raw && !(ix->grouped_pair) && maxm > sorted_len)
-        for (uint32_t w = 1, p = grp.gkey_base; p <= 256 && w <= 8 && w <= maxm - sorted_len; ++w, p *= grp.gkey_base)
-            wsort = w;
-    const uint32_t opts = (ix->grouped_xcd ? kGroupedXcd : 0u) | wsort << 8 | sorted_len << 16;
-    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grp, total, cap, ix->grouped_pair && !raw, opts,
-                                   stream)) !=
-        hipSuccess)
-        return e;
-    if (chain) return hipSuccess;  // (k_emit_chain sums the tiles itself)
-    if (p4)
-        hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(ewg), dim3(256), 0, stream, grp);
-    else
-        hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(ewg), dim3(256), 0, stream, grp);
-    return hipGetLastError();
-}
-
-// Bits per packed symbol for a grouped launch of `grp`, or 0 when it cannot
-// be grouped (a batch without the fixed-length hint); *raw: some batch's
-// patterns do not pack into kGroupPackBits, so the sorted records carry
-// pattern ids alone (FMX_GROUPED_RAW=1 forces that for every launch).
-static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup &grp, bool *raw) {
-    uint32_t bits = 1;
-    while ((1u << bits) < ix->bv.sigma + 1) ++bits;
-    *raw = ix->grouped_raw;
-    for (uint32_t j = 0; j < grp.n; ++j) {
-        if (grp.b[j].stride == 0) return 0;
-        if (grp.b[j].stride * bits > kGroupPackBits) *raw = true;
-    }
-    return bits;
-}
-
 // k_locate's hand-off tag for one launch: a process-wide launch counter
 // through a bijective mix (odd multiplier, splitmix64 finaliser) with a random
 // nonce — distinct for every launch of this process, and unrelated to the
@@ -460,35 +356,244 @@ static uint64_t launch_tag() {
     return z ? z : 1;  // (0: what zeroed memory holds)
 }
 
-// The kernels of a (grouped) locate, one after another on `stream`.
+// Bits per packed symbol for a grouped launch of the ng groups, or 0 when it
+// cannot be grouped (a batch without the fixed-length hint); *raw: some
+// batch's patterns do not pack into kGroupPackBits, so the sorted records
+// carry pattern ids alone (FMX_GROUPED_RAW=1 forces that for every launch).
+static uint32_t group_pack_bits(const fmx_index *ix, const LocateGroup *grps, uint32_t ng, bool *raw) {
+    uint32_t bits = 1;
+    while ((1u << bits) < ix->bv.sigma + 1) ++bits;
+    *raw = ix->grouped_raw;
+    for (uint32_t g = 0; g < ng; ++g)
+        for (uint32_t j = 0; j < grps[g].n; ++j) {
+            if (grps[g].b[j].stride == 0) return 0;
+            if (grps[g].b[j].stride * bits > kGroupPackBits) *raw = true;
+        }
+    return bits;
+}
+
+static uint32_t group_tiles(const LocateGroup &grp) {
+    return grp.tile_begin[grp.n - 1] + (uint32_t)((grp.b[grp.n - 1].npat + 255) / 256);
+}
+
+// k_group_tiles' workgroups of each batch (kEmitTiles tiles of one batch each); their count
+static uint32_t set_emit_begin(LocateGroup &grp) {
+    uint32_t ewg = 0;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        grp.emit_begin[j] = ewg;
+        ewg += (uint32_t)(((grp.b[j].npat + 255) / 256 + kEmitTiles - 1) / kEmitTiles);
+    }
+    return ewg;
+}
+
+static bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
+
+// The tile offsets of batches too large for k_emit's own sum (k_scan), then
+// k_emit: a group's last kernels.  flags bit 1: NarrowRec records (grouped).
+static hipError_t launch_emit(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp, uint32_t tiles,
+                              uint32_t narrow, hipStream_t stream) {
+    const Disp d = dispatch(ix);
+    uint32_t fold = 1;
+    for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
+    if (!fold) {
+        hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold | (narrow ? 2u : 0u), stream);
+}
+
+// One grouped launch over the ng groups' batches (kWsHeader): key counts
+// (per group), their scan, the sorted order (per group: every position of the
+// launch's order, GroupTab), the optional refine and check passes, the search
+// in key order (once), then per group the tile counts and k_emit.  The key
+// counters and the batch table sit in the first batch's workspace.
+static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, LocateGroup *grps, uint32_t ng,
+                                 uint64_t total, uint32_t bits, bool raw, bool chain, hipStream_t stream,
+                                 hipEvent_t mid) {
+    const Disp d = dispatch(ix);
+    const bool p4 = ix->bv.L.pos_bytes == 4;
+    const uint32_t rb = (uint32_t)locate_rec_bytes(ix->bv.L.pos_bytes);
+    uint8_t *ws0 = reinterpret_cast<uint8_t *>(grps[0].b[0].tiles) - kWsHeader;
+    uint32_t *gcount = reinterpret_cast<uint32_t *>(ws0 + 256);
+    GroupTab *d_tab = reinterpret_cast<GroupTab *>(ws0 + kWsGroupTab);
+    // the batch table (what the kernels that see the whole launch read per lane)
+    std::unique_ptr<GroupTab> tab(new (std::nothrow) GroupTab);
+    if (!tab) return hipErrorOutOfMemory;
+    uint32_t gn = 0, vt = 0, maxm = 1, cap = 4;
+    uint64_t first = 0;
+    for (uint32_t g = 0; g < ng; ++g) {
+        LocateGroup &grp = grps[g];
+        grp.vbase = vt;
+        uint32_t chunks = 0;
+        for (uint32_t j = 0; j < grp.n; ++j) {
+            LocateBatch &B = grp.b[j];
+            const uint64_t G = (B.npat + 255) / 256;
+            B.first = first;
+            tab->first[gn] = first;
+            tab->vfirst[gn] = (vt + grp.tile_begin[j]) * 256u;
+            tab->desc[gn] = GroupDesc{reinterpret_cast<uint8_t *>(B.tiles + 2 * G),
+                                      reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + ((B.npat * rb + 15) & ~15ull),
+                                      B.bytes, B.stride, B.rev};
+            ++gn;
+            first += B.npat;
+            grp.chunk_begin[j] = chunks;
+            chunks += (uint32_t)group_chunks(B.npat);
+            maxm = std::max<uint32_t>(maxm, B.stride);
+            cap = std::max<uint32_t>(cap, (B.stride + 3) & ~3u);
+        }
+        vt += group_tiles(grp);
+    }
+    for (uint32_t g = 0; g < ng; ++g) {
+        LocateGroup &grp = grps[g];
+        grp.gcount = gcount;
+        grp.gkey_len = ix->gkey_len;
+        grp.gkey_base = ix->gkey_base;
+        grp.gbits = bits;
+        grp.graw = raw ? 1u : 0u;
+        grp.gtotal = total;
+        grp.gtab = d_tab;
+        grp.gn = gn;
+    }
+    // the key counters start at zero whatever an earlier launch on this
+    // workspace did, and the table is in place: both ordered
+    // before the count pass on the stream
+    hipError_t e = hipMemsetAsync(gcount, 0, 4ull * kGroupBins, stream);
+    if (e != hipSuccess) return e;
+    Stage &stage = const_cast<fmx_index *>(ix)->stage;
+    if ((e = stage.h2d(d_tab->first, tab->first, 8ull * gn, stream)) != hipSuccess ||
+        (e = stage.h2d(d_tab->vfirst, tab->vfirst, 4ull * gn, stream)) != hipSuccess ||
+        (e = stage.h2d(d_tab->desc, tab->desc, sizeof(GroupDesc) * gn, stream)) != hipSuccess)
+        return e;
+    // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the
+    // id-only variant's count pass, for packed records too: the decode, one LDS lookup per byte, bounds
+    // these passes, not their loads — profiles/r4/r4q_*, r4r_*)
+    for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t chunks = grps[g].chunk_begin[grps[g].n - 1] +
+                                (uint32_t)group_chunks(grps[g].b[grps[g].n - 1].npat);
+        hipLaunchKernelGGL((k_group_key<5, false, true>), dim3((chunks + kCountChunks - 1) / kCountChunks),
+                           dim3(1024), 0, stream, qa, grps[g], rb);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(256), 0, stream, gcount);
+    // the place pass holds each pattern in W registers (W = 6 words hold patterns up to 21 bytes at any
+    // alignment, 8 up to 29, 25 up to 97; raw: the key's gkey_len <= 16 bytes in 5)
+    for (uint32_t g = 0; g < ng; ++g) {
+        const LocateGroup &grp = grps[g];
+        const uint32_t chunks = grp.chunk_begin[grp.n - 1] + (uint32_t)group_chunks(grp.b[grp.n - 1].npat);
+        if (raw)
+            hipLaunchKernelGGL((k_group_key<5, true, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+        else if (maxm <= 21)
+            hipLaunchKernelGGL((k_group_key<6, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+        else if (maxm <= 29)
+            hipLaunchKernelGGL((k_group_key<8, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+        else
+            hipLaunchKernelGGL((k_group_key<25, true>), dim3(chunks), dim3(1024), 0, stream, qa, grp, rb);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const bool refined = !raw && total >= ix->group_refine_min;
+    if (refined) {
+        // one workgroup per key from 4,096 patterns per key on average (C2's 25.6 M: every key its own)
+        const uint32_t rg = (uint32_t)std::min<uint64_t>(kGroupBins, std::max<uint64_t>(1, total / 4096));
+        hipLaunchKernelGGL(k_group_refine<0>, dim3(rg), dim3(1024), 0, stream, qa, grps[0], rb);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (ix->group_check) {
+        const uint32_t ord = (uint32_t)((total + 255) / 256);
+        for (uint32_t g = 0; g < ng; ++g)
+            hipLaunchKernelGGL(k_group_check_tally<true>, dim3(group_tiles(grps[g])), dim3(256), 0, stream, qa,
+                               grps[g]);
+        hipLaunchKernelGGL(k_group_check_order, dim3(ord), dim3(256), 0, stream, qa, grps[0], rb);
+        for (uint32_t g = 0; g < ng; ++g)
+            hipLaunchKernelGGL(k_group_check_tally<false>, dim3(group_tiles(grps[g])), dim3(256), 0, stream, qa,
+                               grps[g]);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // each lane unpacks (or, raw, stages) its pattern into `cap` bytes of LDS: the longest batch's length,
+    // 4-byte aligned (raw records longer than kGroupRawStage: the search reads the bytes from HBM, cap 4)
+    if (raw && cap > kGroupRawStage) cap = 4;
+    // (two patterns per lane: packed records only — 512 lanes' staging would not fit LDS)
+    // the in-workgroup sort's symbols: as many after those already in order (the key's, and the refine
+    // pass's as many again) as base^w <= 256 allows (none when every pattern ends within them)
+    const uint32_t sorted_len = ix->gkey_len * (refined ? 2u : 1u);
+    uint32_t wsort = 0;
+    if (ix->grouped_wsort && !raw && !(ix->grouped_pair) && maxm > sorted_len)
+        for (uint32_t w = 1, p = ix->gkey_base; p <= 256 && w <= 8 && w <= maxm - sorted_len; ++w, p *= ix->gkey_base)
+            wsort = w;
+    const uint32_t opts = (ix->grouped_xcd ? kGroupedXcd : 0u) | wsort << 8 | sorted_len << 16;
+    if ((e = d.ops->search_grouped(qa, d.vb, d.rec, grps[0], total, cap, ix->grouped_pair && !raw, opts,
+                                   stream)) != hipSuccess)
+        return e;
+    if (!chain)
+        for (uint32_t g = 0; g < ng; ++g) {
+            const uint32_t ewg = set_emit_begin(grps[g]);
+            if (p4)
+                hipLaunchKernelGGL(k_group_tiles<uint32_t>, dim3(ewg), dim3(256), 0, stream, grps[g]);
+            else
+                hipLaunchKernelGGL(k_group_tiles<uint64_t>, dim3(ewg), dim3(256), 0, stream, grps[g]);
+        }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    (raw ? ix->launches_grouped_raw : ix->launches_grouped).fetch_add(1, std::memory_order_relaxed);
+    if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
+    for (uint32_t g = 0; g < ng; ++g) {
+        if (chain) {
+            e = d.ops->emit_chain(qa, d.vb, d.rec, grps[g], group_tiles(grps[g]), launch_tag(), ix->fused_late_ticks,
+                                  stream);
+        } else {
+            e = launch_emit(ix, qa, grps[g], group_tiles(grps[g]), 1u, stream);
+        }
+        if (e != hipSuccess) return e;
+    }
+    if (chain) ix->launches_chained.fetch_add(1, std::memory_order_relaxed);
+    return hipSuccess;
+}
+
+// Whether the ng groups (every batch with its fields filled, tile_begin[0] =
+// 0 in each) run as one grouped launch: the index has a key, every batch the
+// fixed-length hint, the launch at least grouped_min patterns (grouped_raw_min
+// when the records must be id-only), the faithful search, and 32-bit pattern
+// ids.
+static bool is_grouped(const fmx_index *ix, const QueryArgs &qa, const LocateGroup *grps, uint32_t ng, uint32_t sb,
+                       uint64_t *total, uint32_t *bits, bool *raw) {
+    uint64_t n = 0, tiles = 0;
+    for (uint32_t g = 0; g < ng; ++g) {
+        if (grps[g].tile_ctr) return false;
+        for (uint32_t j = 0; j < grps[g].n; ++j) n += grps[g].b[j].npat;
+        tiles += group_tiles(grps[g]);
+    }
+    *total = n;
+    *bits = group_pack_bits(ix, grps, ng, raw);
+    return ix->gkey_len != 0 && *bits != 0 && n >= (*raw ? ix->grouped_raw_min : ix->grouped_min) &&
+           search_var(qa, sb) == kVarFaithful && tiles * 256u <= 0xFFFFFFFFull;
+}
+
+// The kernels of a locate of one group, one after another on `stream`.
 static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateGroup &grp, uint32_t tiles,
                                uint32_t sb, hipStream_t stream, hipEvent_t mid = nullptr) {
     const Disp d = dispatch(ix);
     uint64_t total = 0;
-    uint32_t ewg = 0;  // k_group_tiles workgroups (kEmitTiles tiles of one batch each); k_emit: one per tile
-    for (uint32_t j = 0; j < grp.n; ++j) {
-        grp.b[j].first = total;
-        total += grp.b[j].npat;
-        grp.emit_begin[j] = ewg;
-        ewg += (uint32_t)(((grp.b[j].npat + 255) / 256 + kEmitTiles - 1) / kEmitTiles);
-    }
+    uint32_t bits = 0;
     bool raw = false;
-    const uint32_t bits = group_pack_bits(ix, grp, &raw);
-    const bool grouped = ix->gkey_len != 0 && bits != 0 && total >= (raw ? ix->grouped_raw_min : ix->grouped_min) &&
-                         !grp.tile_ctr &&
-                         search_var(qa, sb) == kVarFaithful && (uint64_t)tiles * 256u <= 0xFFFFFFFFull;
-    // in launch order, batches of at most kFoldTiles tiles of short fixed-length patterns: one kernel
-    // (k_locate); grouped, batches of at most kFoldTiles tiles: k_emit_chain ends the launch — both
-    // unless the stream is being captured (a replayed graph would reuse the launch's tag)
     bool small = true;
     for (uint32_t j = 0; small && j < grp.n; ++j) small = (grp.b[j].npat + 255) / 256 <= kFoldTiles;
-    bool fused = !grouped && small && ix->fused && !grp.tile_ctr && tiles <= ix->fused_max_tiles;
-    for (uint32_t j = 0; fused && j < grp.n; ++j) fused = grp.b[j].stride != 0 && grp.b[j].stride <= kFusedMaxLen;
-    bool chain = grouped && small && ix->emit_chain;
-    if (fused || chain) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) fused = chain = false;
+    if (is_grouped(ix, qa, &grp, 1, sb, &total, &bits, &raw)) {
+        // grouped, batches of at most kFoldTiles tiles: k_emit_chain may end the launch (FMX_EMIT_CHAIN=1)
+        const bool chain = small && ix->emit_chain && !stream_capturing(stream);
+        return launch_grouped(ix, qa, &grp, 1, total, bits, raw, chain, stream, mid);
     }
+    uint64_t first = 0;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        grp.b[j].first = first;
+        first += grp.b[j].npat;
+    }
+    // in launch order, batches of at most kFoldTiles tiles of short fixed-length patterns: one kernel
+    // (k_locate), unless the stream is being captured (a replayed graph would reuse the launch's tag)
+    bool fused = small && ix->fused && !grp.tile_ctr && tiles <= ix->fused_max_tiles;
+    for (uint32_t j = 0; fused && j < grp.n; ++j) fused = grp.b[j].stride != 0 && grp.b[j].stride <= kFusedMaxLen;
+    if (fused && stream_capturing(stream)) fused = false;
     hipError_t e;
     if (fused) {
         if ((e = d.ops->locate(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, launch_tag(),
@@ -499,24 +604,10 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
         // (timing: the whole launch is the first phase)
         return mid ? hipEventRecord(mid, stream) : hipSuccess;
     }
-    e = grouped ? launch_grouped_search(ix, qa, grp, ewg, total, sb, bits, raw, chain, stream)
-                : d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream);
-    if (e != hipSuccess) return e;
-    (grouped ? (raw ? ix->launches_grouped_raw : ix->launches_grouped) : ix->launches_ordered)
-        .fetch_add(1, std::memory_order_relaxed);
+    if ((e = d.ops->search(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, stream)) != hipSuccess) return e;
+    ix->launches_ordered.fetch_add(1, std::memory_order_relaxed);
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
-    if (chain) {
-        ix->launches_chained.fetch_add(1, std::memory_order_relaxed);
-        return d.ops->emit_chain(qa, d.vb, d.rec, grp, tiles, launch_tag(), ix->fused_late_ticks, stream);
-    }
-    uint32_t fold = 1;
-    for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
-    if (!fold) {
-        hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    // (k_emit's flags: bit 0 fold, bit 1 NarrowRec records from the grouped search)
-    return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold | (grouped ? 2u : 0u), stream);
+    return launch_emit(ix, qa, grp, tiles, 0u, stream);
 }
 
 hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint64_t *d_offsets, uint64_t n,
@@ -536,18 +627,55 @@ hipError_t launch_locate(const fmx_index *ix, const uint8_t *d_bytes, const uint
     return launch_split(ix, qa, grp, (uint32_t)((n + 255) / 256), stage_bytes_for(flags), stream);
 }
 
+static hipError_t check_group(const LocateGroup &grp, uint64_t *tiles) {
+    if (grp.n == 0 || grp.n > kMaxGroup || grp.tile_begin[0] != 0) return hipErrorInvalidValue;
+    uint64_t t = 0;
+    for (uint32_t j = 0; j < grp.n; ++j) {
+        if (grp.b[j].npat == 0 || grp.tile_begin[j] != t) return hipErrorInvalidValue;
+        t += (grp.b[j].npat + 255) / 256;
+    }
+    if (t > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    *tiles = t;
+    return hipSuccess;
+}
+
 hipError_t launch_locate_group(const fmx_index *ix, LocateGroup &grp, uint32_t stage_flags,
                                uint32_t *status, hipStream_t stream, hipEvent_t mid) {
     QueryArgs qa = ix->qa;
     qa.status = status;
-    if (grp.n == 0 || grp.n > kMaxGroup || grp.tile_begin[0] != 0) return hipErrorInvalidValue;
     uint64_t tiles = 0;
-    for (uint32_t j = 0; j < grp.n; ++j) {
-        if (grp.b[j].npat == 0 || grp.tile_begin[j] != tiles) return hipErrorInvalidValue;
-        tiles += (grp.b[j].npat + 255) / 256;
-    }
-    if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipError_t e = check_group(grp, &tiles);
+    if (e != hipSuccess) return e;
     return launch_split(ix, qa, grp, (uint32_t)tiles, stage_bytes_for(stage_flags), stream, mid);
+}
+
+hipError_t launch_locate_groups(const fmx_index *ix, LocateGroup *grps, uint32_t ng, uint32_t stage_flags,
+                                uint32_t *status, hipStream_t stream, hipEvent_t mid) {
+    if (ng == 0 || (uint64_t)ng * kMaxGroup > kMaxMega) return hipErrorInvalidValue;
+    if (ng == 1) return launch_locate_group(ix, grps[0], stage_flags, status, stream, mid);
+    QueryArgs qa = ix->qa;
+    qa.status = status;
+    const uint32_t sb = stage_bytes_for(stage_flags);
+    uint64_t tiles[kMaxMega / kMaxGroup];
+    hipError_t e;
+    for (uint32_t g = 0; g < ng; ++g)
+        if ((e = check_group(grps[g], &tiles[g])) != hipSuccess) return e;
+    uint64_t total = 0;
+    uint32_t bits = 0;
+    bool raw = false;
+    if (is_grouped(ix, qa, grps, ng, sb, &total, &bits, &raw)) {
+        bool small = true;
+        for (uint32_t g = 0; g < ng; ++g)
+            for (uint32_t j = 0; small && j < grps[g].n; ++j) small = (grps[g].b[j].npat + 255) / 256 <= kFoldTiles;
+        const bool chain = small && ix->emit_chain && !stream_capturing(stream);
+        return launch_grouped(ix, qa, grps, ng, total, bits, raw, chain, stream, mid);
+    }
+    // in launch order: one launch per group (timing: the last group's search ends the first phase)
+    for (uint32_t g = 0; g < ng; ++g)
+        if ((e = launch_split(ix, qa, grps[g], (uint32_t)tiles[g], sb, stream, g + 1 == ng ? mid : nullptr)) !=
+            hipSuccess)
+            return e;
+    return hipSuccess;
 }
 
 uint64_t locate_rec_bytes(uint32_t pos_bytes) {

@@ -680,3 +680,63 @@ def test_chained_grouped_emit_simt(pkg, O, fused, monkeypatch, seed):
     info = ix.info()
     assert info["launches_grouped"] == info["launches_chained"] == 2, info
     ix.close()
+
+
+@pytest.mark.parametrize("grouped", ["1", "0"])
+def test_launch_of_many_groups_simt(pkg, O, simt, monkeypatch, grouped):
+    """More than 256 batches in one fmx_locate_group_async call (700: three
+    kernel-argument groups).  Grouped: ONE grouped launch over all of them —
+    the key counts and the place pass per group, the scan, the refine and
+    check passes and the search once over the launch's whole order (its batch
+    table, GroupTab, in the first batch's workspace), tiles and emit per
+    group; in launch order: one launch per group.  Fixed-length batches of
+    1-60 patterns, lengths 2..29, every third reversed, random-byte
+    workspaces, twice, against the oracle."""
+    monkeypatch.setenv("FMX_GROUPED", grouped)
+    monkeypatch.setenv("FMX_GROUP_CHECK", "1")
+    monkeypatch.setenv("FMX_GROUP_REFINE_MIN", "1")
+    simt.simt_config(515 + len(grouped), 0.5)
+    rng = np.random.default_rng(71)
+    table = table_from_symbols([b"A", b"C", b"G", b"T", b"N"])
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20_000).astype(np.uint8)
+    blob = O.build(text.tobytes(), 5, O.layout(4, 3, 64), 3, 2, table)
+    orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    sizes = [int(x) for x in np.random.default_rng(8).integers(1, 60, size=700)]
+    bats, jobs = [], []
+    for bi, n in enumerate(sizes):
+        rev, m = bi % 3 == 2, 2 + (bi * 11) % 28
+        starts = rng.integers(0, text.size - m, size=n)
+        pats = [text[s:s + m].tobytes() for s in starts]
+        data, offsets = pkg.pack_patterns(pats)
+        want = orc.locate_batch(data, offsets)
+        q = [p[::-1] for p in pats] if rev else pats
+        data, offsets = pkg.pack_patterns(q)
+        cap = int(want[1].size) + 8
+        ws = ix.locate_workspace_size(n)
+        b = dict(n=n, want=want, data=np.concatenate([data, np.zeros(16, np.uint8)]),
+                 off=offsets.view(np.int64).copy(), loff=rng.integers(0, 2**62, size=n + 1).astype(np.int64),
+                 locs=rng.integers(0, 2**31, size=cap).astype(np.int32), need=np.zeros(1, np.int64),
+                 cnt=rng.integers(0, 2**31, size=n).astype(np.int32),
+                 ws=rng.integers(0, 256, size=ws).astype(np.uint8))
+        jobs.append(ix.locate_job(b["data"].ctypes.data, b["off"].ctypes.data, n, b["loff"].ctypes.data,
+                                  b["locs"].ctypes.data, cap, b["need"].ctypes.data, b["ws"].ctypes.data, ws,
+                                  d_counts=b["cnt"].ctypes.data, reversed=rev, stage_kb=max(1, -(-256 * m // 1024)),
+                                  fixed_len=m))
+        bats.append(b)
+    q = ix.job_queue(jobs)
+    for rep in range(2):
+        ix.locate_group_async(q)
+        ix.sync()
+        for bi, b in enumerate(bats):
+            wo, wl = b["want"]
+            assert np.array_equal(b["loff"].view(np.uint64), wo), f"rep {rep} batch {bi}: offsets"
+            assert np.array_equal(b["locs"][:wl.size].view(np.uint32), wl), f"rep {rep} batch {bi}: locations"
+            assert int(b["need"][0]) == wl.size
+            assert np.array_equal(b["cnt"].view(np.uint32), np.diff(wo).astype(np.uint32))
+    info = ix.info()
+    if grouped == "1":
+        assert info["launches_grouped"] == 2 and info["launches_ordered"] == 0, info
+    else:
+        assert info["launches_grouped"] == 0 and info["launches_ordered"] == 6, info
+    ix.close()
