@@ -37,6 +37,8 @@
 #   fusedtest  only tests/test_gpu_fused.py (the fused launch, k_locate)
 #   chainab  C2 (grouped) ended by k_emit_chain vs k_group_tiles + k_emit (FMX_EMIT_CHAIN=0), alternating twice
 #   psweep   C2 at 100k / 200k / 400k patterns per batch (256 batches per launch: 25.6 / 51.2 / 102.4 M per launch)
+#   groupedtest  tests/test_gpu_grouped.py and tests/test_gpu_fused.py only
+#   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   fusedab  the fused launch vs the two-kernel path (FMX_FUSED=0): single batch, C1, C4, alternating twice;
 #            then the single-batch kernel trace of the fused build
 # Every step has its own time limit; the first failing step ends the run.
@@ -189,6 +191,13 @@ for step in "$@"; do
             for r in 1 2; do
                 run "chain_on_$r" 300 $B || exit 1
                 FMX_EMIT_CHAIN=0 run "chain_off_$r" 300 $B || exit 1
+            done ;;
+        groupedtest) run pytest_grouped 900 python -u -m pytest tests/test_gpu_grouped.py tests/test_gpu_fused.py -x -v \
+                --timeout 300 --timeout-method thread || exit 1 ;;
+        megab)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                for g in 256 512 1024; do run "mega_g${g}_$r" 400 $B --group $g || exit 1; done
             done ;;
         psweep)
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
