@@ -231,8 +231,9 @@ def test_chained_grouped_launches(pkg, O, monkeypatch, chain):
     counts handed from tile to tile inside the kernel; FMX_EMIT_CHAIN=0: the
     k_group_tiles + k_emit pair): 300 fixed-length batches of 1-3,000
     patterns, lengths 8..28, every third reversed, random-byte workspaces and
-    outputs, three rounds: every batch against the oracle, and the launch
-    counters show which ending ran."""
+    outputs, three rounds (each one grouped launch over two kernel-argument
+    groups): every batch against the oracle, and the launch counters show
+    which ending ran."""
     import torch
     rng, text, blob = c2_like(pkg, O, 4_000_000, 54)
     orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
@@ -277,6 +278,7 @@ def test_chained_grouped_launches(pkg, O, monkeypatch, chain):
                 f"rep {rep} batch {bi}: locations"
             assert np.array_equal(b["cnt"].cpu().numpy().view(np.uint32), np.diff(wo).astype(np.uint32))
     info = ix.info()
-    assert info["launches_grouped"] == 6 and info["launches_ordered"] == 0, info
-    assert info["launches_chained"] == (6 if chain == "1" else 0), info
+    # (300 batches: ONE grouped launch per round, over two kernel-argument groups)
+    assert info["launches_grouped"] == 3 and info["launches_ordered"] == 0, info
+    assert info["launches_chained"] == (3 if chain == "1" else 0), info
     ix.close()
