@@ -601,7 +601,16 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     __shared__ uint8_t s_dig[kMaxSigma];
     __shared__ uint32_t s_pw[32];
     __shared__ uint32_t hist[kGroupBins];
+    // (place) the launch's batches (GroupTab): sorted positions before each (32-bit: a launch's pattern ids
+    // are), and where each holds its share of the sorted order
+    __shared__ uint32_t s_first[PLACE ? kMaxMega : 1];
+    __shared__ U4 *s_sorted[PLACE ? kMaxMega : 1];
     const uint32_t t = threadIdx.x;
+    if constexpr (PLACE)
+        for (uint32_t j = t; j < grp.gn; j += T) {
+            s_first[j] = (uint32_t)grp.gtab->first[j];
+            s_sorted[j] = reinterpret_cast<U4 *>(grp.gtab->desc[j].sorted);
+        }
     if (t < 256) s_enc[t] = a.tab->enc[t];
     if (t < (uint32_t)kMaxSigma) s_dig[t] = a.tab->dig[t] == kNoDigit ? 0 : a.tab->dig[t];  // (absent: occurs nowhere)
     if (t == 0) {
@@ -731,10 +740,8 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
                 atomicOr(a.status, kStatusGroup);
                 continue;
             }
-            // the batch holding sorted position sp (the launch's batch table, GroupTab)
-            const GroupTab &gt = *grp.gtab;
-            const uint32_t js = lds_upper(gt.first, grp.gn, sp);
-            reinterpret_cast<U4 *>(gt.desc[js].sorted)[sp - gt.first[js]] = rec_r[p];
+            const uint32_t js = lds_upper(s_first, grp.gn, (uint32_t)sp);  // (the batch holding position sp)
+            s_sorted[js][sp - s_first[js]] = rec_r[p];
         }
     }
 }
@@ -910,6 +917,10 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     __shared__ Tables<P> s;
     __shared__ uint8_t s_dig[kMaxSigma + 1];  // (wsort) symbol -> digit; sigma (past the pattern's start) -> 0
     __shared__ uint64_t s_wscan[4];
+    // the launch's batches (GroupTab), for the lanes' binary searches: sorted positions and pattern ids
+    // before each (32-bit: a launch's are), and each one's pattern length
+    __shared__ uint32_t s_first[kMaxMega], s_vfirst[kMaxMega];
+    __shared__ uint16_t s_stride[kMaxMega];
     const uint32_t wsort = K == 1 && !grp.graw ? (opts >> 8) & 0xffu : 0u, xcd = opts & kGroupedXcd;
     const uint32_t wskip = opts >> 16;
     FMX_DYN_LDS(s_pat);  // 256 K x cap B of symbols (cap >= every batch's length), then the k-mer table
@@ -917,8 +928,12 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     if (threadIdx.x <= (uint32_t)kMaxSigma)
         s_dig[threadIdx.x] =
             threadIdx.x < a.sigma && a.tab->dig[threadIdx.x] != kNoDigit ? a.tab->dig[threadIdx.x] : 0;
-    // (the launch's batches, GroupTab: each lane finds its pattern's batch by binary searches there)
     const GroupTab &gt = *grp.gtab;
+    for (uint32_t j = threadIdx.x; j < grp.gn; j += 256) {
+        s_first[j] = (uint32_t)gt.first[j];
+        s_vfirst[j] = gt.vfirst[j];
+        s_stride[j] = (uint16_t)gt.desc[j].stride;
+    }
     __syncthreads();
     // xcd: workgroup b takes chunk start(b % 8) + b / 8, so that (under the
     // round-robin placement of workgroups over the 8 XCDs, which only speed
@@ -945,13 +960,13 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         pv[q].enc = s.enc;
         pv[q].sym = dst;
         if (!live[q]) continue;
-        const uint32_t js = lds_upper(gt.first, grp.gn, sp);
-        U4 e = reinterpret_cast<const U4 *>(gt.desc[js].sorted)[sp - gt.first[js]];
+        const uint32_t js = lds_upper(s_first, grp.gn, (uint32_t)sp);
+        U4 e = reinterpret_cast<const U4 *>(gt.desc[js].sorted)[sp - s_first[js]];
         if (K == 1 && wsort && (uint64_t)chunk * 256u + 256u <= total) {  // (workgroup-uniform: all lanes live)
             uint32_t *hist = reinterpret_cast<uint32_t *>(s_pat);
             U4 *stage = reinterpret_cast<U4 *>(s_pat + 1024);
             const uint32_t t = threadIdx.x, base = grp.gkey_base;
-            const uint32_t m = gt.desc[lds_upper(gt.vfirst, grp.gn, e.w)].stride;
+            const uint32_t m = s_stride[lds_upper(s_vfirst, grp.gn, e.w)];
             uint32_t k2 = 0;
             for (uint32_t d = 0; d < wsort; ++d) {
                 const uint32_t back = wskip + d;  // 0 = the pattern's last symbol
@@ -971,13 +986,13 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
             __syncthreads();  // (the stage is s_pat: every lane has its record before any unpacks)
         }
         const uint32_t v = e.w;
-        const uint32_t jb = lds_upper(gt.vfirst, grp.gn, v);
-        const GroupDesc dj = gt.desc[jb];
+        const uint32_t jb = lds_upper(s_vfirst, grp.gn, v);
+        const GroupDesc &dj = gt.desc[jb];  // (recs: written at the end; bytes, rev: id-only records)
         recp[q] = dj.recs;
-        pi[q] = (uint64_t)(v - gt.vfirst[jb]);
-        pv[q].m = dj.stride;
+        pi[q] = (uint64_t)(v - s_vfirst[jb]);
+        pv[q].m = s_stride[jb];
         if (grp.graw) {
-            const uint32_t m = dj.stride;
+            const uint32_t m = s_stride[jb];
             const uint8_t *src = dj.bytes + pi[q] * m;
             if (cap >= m) {
                 // the pattern's bytes (input order) into its cap bytes of LDS,
@@ -1008,7 +1023,7 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
                 pv[q].sym = nullptr;
             }
         } else {
-            grouped_unpack<P>(e, dj.stride, grp.gbits, dst);
+            grouped_unpack<P>(e, s_stride[jb], grp.gbits, dst);
         }
     }
     P lo_r[K], hi_r[K], rloc[K];
