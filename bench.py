@@ -83,12 +83,13 @@ CONFIGS = {
     "c1": dict(text_len=1_000_000, alphabet=b"ACGT", symbols=[b"Aa", b"Cc", b"Gg", b"Tt"], pos=4, planes=2,
                vec=64, k=3, sr=2, patterns=1_000, m=20, total=0, group=256, streams=2,
                desc="C1: 1 Mbp ACGT, 1,000 x 20 bp, u32/Block2<u64>, sr 2, k 3"),
-    # configs[1]: the headline (metric quoted on it).  256 batches per launch (one launch group
-    # per stream, 512 distinct batches): a grouped launch of 25.6 M patterns shares more of its
-    # first LF steps than one of 12.8 M, 3.2 M, 1.6 M or 0.8 M (3.42 vs 3.28 vs 2.84 vs ~2.7 vs
-    # ~2.6e9; launch order ~2.58; profiles/r3/narrow, profiles/r3/grouped/r3ls2, r3g32, r3g6)
+    # configs[1]: the headline (metric quoted on it).  1,024 batches per launch (one launch group
+    # per stream, 2,048 distinct batches): a grouped launch of 102.4 M patterns shares more of its
+    # first LF steps than one of 51.2 M or 25.6 M (4.04 vs 3.92 vs 3.60-3.66e9, profiles/r5/r5y_mega_*;
+    # and 25.6 M more than 12.8 M, 3.2 M, 1.6 M or 0.8 M: 3.42 vs 3.28 vs 2.84 vs ~2.7 vs ~2.6e9 in
+    # round 3; launch order ~2.58; profiles/r3/narrow, profiles/r3/grouped/r3ls2, r3g32, r3g6)
     "c2": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
-               patterns=100_000, m=20, total=0, group=256,
+               patterns=100_000, m=20, total=0, group=1024,
                desc="C2: 1 Gbp ACGT (ACGTN, N wildcard), 100,000 x 20 bp per GPU, u32/Block3<u64>, sr 2, k 3"),
     # configs[2]: 10 M patterns sharded over the GPUs
     "c3": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,

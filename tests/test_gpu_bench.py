@@ -89,8 +89,8 @@ def test_rccl_world1_weak_gather():
     """c2-shaped weak scaling under torchrun with one RCCL rank: each launch
     group's counts and locations all-gathered by RCCL inside the timed step;
     the assembled results hold this rank's part intact."""
-    p = run_bench(["--config", "c2", "--text-len", "20000000", "--patterns", "20000", "--steps", "16",
-                   "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
+    p = run_bench(["--config", "c2", "--text-len", "20000000", "--patterns", "20000", "--group", "64", "--steps",
+                   "16", "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
                   env_extra={"FMX_BENCH_DIST": "1"}, torchrun=1)
     assert p.returncode == 0, p.stderr[-3000:]
     r = last_json(p.stdout)
@@ -133,7 +133,7 @@ def test_gloo_two_ranks_weak_gather():
     group's results are all-gathered inside the timed step (one collective
     per launch, exactly sized slabs), the job assembled on the device holds
     this rank's part intact, and the padding stays under 1.25x."""
-    p = run_bench(["--gpus", "2", "--config", "c2", "--text-len", "20000000", "--patterns", "20000",
+    p = run_bench(["--gpus", "2", "--config", "c2", "--text-len", "20000000", "--patterns", "20000", "--group", "64",
                    "--steps", "16", "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
                   env_extra={"FMX_BENCH_BACKEND": "gloo"})
     assert p.returncode == 0, p.stderr[-3000:]
