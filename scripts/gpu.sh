@@ -230,6 +230,7 @@ for step in "$@"; do
                 --kernel-trace -d "$OUT/pmc_ea" -o run --output-format csv -- python3 -u bench.py $P || exit 1
             run pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run \
                 --output-format csv -- python3 -u bench.py $P || exit 1
+            [ "${PMC_SKIP_TCC:-0}" = 1 ] && continue
             run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$OUT/pmc_tcc" -o run \
                 --output-format csv -- python3 -u bench.py $P || exit 1 ;;
         configs)

@@ -19,6 +19,8 @@ def main():
     tag, prefix = sys.argv[1], sys.argv[2]
     g = os.path.join(ROOT, "gpurun_out", tag)
     for p in ("fetch", "ea", "write", "tcc"):
+        if not os.path.isdir(os.path.join(g, f"pmc_{p}")):
+            continue  # (the TCC pass is optional)
         path = None
         for root, _, files in os.walk(os.path.join(g, f"pmc_{p}")):
             for f in files:

@@ -69,7 +69,9 @@ def main():
     fetch, fetch_s, nl = sums(csv_of(os.path.join(g, "pmc_fetch")))
     ea, ea_s, nl2 = sums(csv_of(os.path.join(g, "pmc_ea")))
     wr, wr_s, nl3 = sums(csv_of(os.path.join(g, "pmc_write")))
-    tcc, tcc_s, nl4 = sums(csv_of(os.path.join(g, "pmc_tcc")))
+    # (the TCC hit / miss pass is optional: PMC_SKIP_TCC=1 in scripts/gpu.sh)
+    has_tcc = os.path.isdir(os.path.join(g, "pmc_tcc"))
+    tcc, tcc_s, nl4 = sums(csv_of(os.path.join(g, "pmc_tcc"))) if has_tcc else ({}, {}, 1)
 
     def reads(e, n):
         n64, n128, nreq = e["TCC_EA0_RDREQ_64B_sum"] / n, e["TCC_EA0_RDREQ_128B_sum"] / n, e["TCC_EA0_RDREQ_sum"] / n
@@ -91,14 +93,15 @@ def main():
         "fabric_bytes_per_launch": rd,
         "write_bytes_per_launch": wb,
         "traffic_bytes_per_launch": rd + wb,
-        "l2_hit_rate": tcc["TCC_HIT_sum"] / max(tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"], 1),
-        "l2_requests_per_pattern": (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]) / nl4 / ppl,
+        "l2_hit_rate": tcc["TCC_HIT_sum"] / max(tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"], 1) if has_tcc else None,
+        "l2_requests_per_pattern": (tcc["TCC_HIT_sum"] + tcc["TCC_MISS_sum"]) / nl4 / ppl if has_tcc else None,
         # the search kernel alone
         "search_kernel": {
             "fabric_requests_per_launch": sreq, "fabric_bytes_per_launch": srd, "write_bytes_per_launch": swb,
             "fetch_size_x2_bytes_per_launch": 2 * fetch_s["FETCH_SIZE"] * 1024 / nl,
             "fabric_requests_per_pattern": sreq / ppl, "traffic_bytes_per_pattern": (srd + swb) / ppl,
-            "l2_hit_rate": tcc_s["TCC_HIT_sum"] / max(tcc_s["TCC_HIT_sum"] + tcc_s["TCC_MISS_sum"], 1),
+            "l2_hit_rate": (tcc_s["TCC_HIT_sum"] / max(tcc_s["TCC_HIT_sum"] + tcc_s["TCC_MISS_sum"], 1)
+                            if has_tcc else None),
         },
     }
     run["fabric_bytes_per_pattern"] = rd / ppl
