@@ -406,6 +406,32 @@ static hipError_t launch_emit(const fmx_index *ix, const QueryArgs &qa, const Lo
     return d.ops->emit(qa, d.vb, d.rec, grp, tiles, fold | (narrow ? 2u : 0u), stream);
 }
 
+// Host bytes into HBM in stream order through kernel arguments (a grouped
+// launch's batch table): no DMA from host memory and no host wait on the
+// GPU in an asynchronous launch — the pinned stage's buffers, shared by every
+// stream, would make one stream's launch wait for another's earlier copy (and
+// rocprofv3's counter passes hung at that wait, profiles/r5/r5z*).  A few
+// one-workgroup kernels of kPutChunk bytes each (per-lane reads of the
+// kernel argument: ~10 us each, r5g_kernarg_cost).
+constexpr uint32_t kPutChunk = 24576;
+struct PutChunk {
+    uint64_t n;
+    uint8_t b[kPutChunk];
+};
+__global__ __launch_bounds__(256) void k_put_bytes(uint8_t *__restrict__ dst, const PutChunk c) {
+    for (uint64_t i = threadIdx.x; i < c.n; i += 256) dst[i] = c.b[i];
+}
+static hipError_t put_bytes(void *dst, const void *src, uint64_t n, hipStream_t s) {
+    std::unique_ptr<PutChunk> c(new (std::nothrow) PutChunk);
+    if (!c) return hipErrorOutOfMemory;
+    for (uint64_t o = 0; o < n; o += kPutChunk) {
+        c->n = std::min<uint64_t>(kPutChunk, n - o);
+        memcpy(c->b, static_cast<const uint8_t *>(src) + o, c->n);
+        hipLaunchKernelGGL(k_put_bytes, dim3(1), dim3(256), 0, s, static_cast<uint8_t *>(dst) + o, *c);
+    }
+    return hipGetLastError();
+}
+
 // One grouped launch over the ng groups' batches (kWsHeader): key counts
 // (per group), their scan, the sorted order (per group: every position of the
 // launch's order, GroupTab), the optional refine and check passes, the search
@@ -463,10 +489,9 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
     // before the count pass on the stream
     hipError_t e = hipMemsetAsync(gcount, 0, 4ull * kGroupBins, stream);
     if (e != hipSuccess) return e;
-    Stage &stage = const_cast<fmx_index *>(ix)->stage;
-    if ((e = stage.h2d(d_tab->first, tab->first, 8ull * gn, stream)) != hipSuccess ||
-        (e = stage.h2d(d_tab->vfirst, tab->vfirst, 4ull * gn, stream)) != hipSuccess ||
-        (e = stage.h2d(d_tab->desc, tab->desc, sizeof(GroupDesc) * gn, stream)) != hipSuccess)
+    if ((e = put_bytes(d_tab->first, tab->first, 8ull * gn, stream)) != hipSuccess ||
+        (e = put_bytes(d_tab->vfirst, tab->vfirst, 4ull * gn, stream)) != hipSuccess ||
+        (e = put_bytes(d_tab->desc, tab->desc, sizeof(GroupDesc) * gn, stream)) != hipSuccess)
         return e;
     // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the
     // id-only variant's count pass, for packed records too: the decode, one LDS lookup per byte, bounds
