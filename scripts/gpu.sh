@@ -222,6 +222,16 @@ for step in "$@"; do
                 python3 -u bench.py --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1
             run trace_default 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace2" -o run --output-format csv -- \
                 python3 -u bench.py --no-cpu || exit 1 ;;
+        pmcw)  # the WRITE_SIZE pass alone (a pass that hangs can be re-run on its own)
+            P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+            run pmc_write 170 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run \
+                --output-format csv -- python3 -u bench.py $P || exit 1 ;;
+        pmcfe)  # the FETCH_SIZE and request-split passes
+            P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+            run pmc_fetch 170 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \
+                --output-format csv -- python3 -u bench.py $P || exit 1
+            run pmc_ea 170 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
+                --kernel-trace -d "$OUT/pmc_ea" -o run --output-format csv -- python3 -u bench.py $P || exit 1 ;;
         pmc)
             P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
             run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \
