@@ -247,17 +247,34 @@ class Workload:
         self.stage_kb = min(56, -(-256 * m // 1024))  # FMX_HINT_STAGE_KB: a tile spans 256 * m bytes
         self.fixed = fixed
         self.batches = []
+        # one allocation per kind, each batch a view (a few kernels instead of ~10 per batch: 2,048 batches
+        # under rocprofv3's counter passes, which serialise every dispatch, took minutes): the patterns back
+        # to back (+64 B: the key passes read whole words), offsets shared by batches of one size, the
+        # workspaces 256-B aligned
+        sizes = [int(st.numel()) for st in starts_list]
+        caps = [b + b // 8 + 4096 for b in sizes]
+        wss = [-(-ix.locate_workspace_size(max(b, 1)) // 256) * 256 for b in sizes]
+        pat_all = torch.zeros(sum(sizes) * m + 64, dtype=torch.uint8, device=dev)
+        if sizes:
+            pat_all[:sum(sizes) * m] = cut_patterns(torch, d_text, torch.cat(starts_list), m)
+        loff_all = torch.zeros(sum(sizes) + len(sizes), dtype=torch.int64, device=dev)
+        need_all = torch.zeros(max(len(sizes), 1), dtype=torch.int64, device=dev)
+        ws_all = torch.zeros(sum(wss) + 256, dtype=torch.uint8, device=dev)
+        ws_base = (-ws_all.data_ptr()) % 256
+        cnt_all = torch.zeros(sum(max(b, 1) for b in sizes), dtype=self.pdt, device=dev)
+        locs_all = torch.zeros(sum(caps), dtype=self.pdt, device=dev)
+        offs = {}
+        po = lo = wo = co = ao = 0
         for k, starts in enumerate(starts_list):
-            b = int(starts.numel())
+            b, cap, wsz = sizes[k], caps[k], wss[k]
             g, j = divmod(k, GR)
-            cap = b + b // 8 + 4096
-            bt = dict(k=k, group=g, slot=j, n=b, starts=starts, pat=cut_patterns(torch, d_text, starts, m),
-                      off=(torch.arange(b + 1, device=dev, dtype=torch.int64) * m).contiguous(),
-                      loff=torch.zeros(b + 1, dtype=torch.int64, device=dev),
-                      need=torch.zeros(1, dtype=torch.int64, device=dev),
-                      ws_t=torch.zeros(ix.locate_workspace_size(max(b, 1)), dtype=torch.uint8, device=dev),
-                      cnt=torch.zeros(max(b, 1), dtype=self.pdt, device=dev),
-                      locs=torch.zeros(cap, dtype=self.pdt, device=dev), cap=cap)
+            if b not in offs:
+                offs[b] = (torch.arange(b + 1, device=dev, dtype=torch.int64) * m).contiguous()
+            bt = dict(k=k, group=g, slot=j, n=b, starts=starts, pat=pat_all[po:po + b * m], off=offs[b],
+                      loff=loff_all[lo:lo + b + 1], need=need_all[k:k + 1],
+                      ws_t=ws_all[ws_base + wo:ws_base + wo + wsz], cnt=cnt_all[co:co + max(b, 1)],
+                      locs=locs_all[ao:ao + cap], cap=cap)
+            po, lo, wo, co, ao = po + b * m, lo + b + 1, wo + wsz, co + max(b, 1), ao + cap
             self.batches.append(bt)
         self.n_groups = -(-len(self.batches) // GR)
         self.bind()
@@ -609,12 +626,11 @@ def main():
     strong = total > 0
 
     def weak_starts(nbatches):
-        out = []
-        for bi in range(nbatches):
-            pg = torch.Generator(device=dev)
-            pg.manual_seed(args.seed * 1000 + 7 + 100003 * bi + 7919 * rank)
-            out.append(torch.randint(0, n - m + 1, (B,), device=dev, dtype=torch.int64, generator=pg))
-        return out
+        # (one draw for all of this rank's batches; each batch a view)
+        pg = torch.Generator(device=dev)
+        pg.manual_seed(args.seed * 1000 + 7 + 7919 * rank)
+        allst = torch.randint(0, n - m + 1, (nbatches, B), device=dev, dtype=torch.int64, generator=pg)
+        return [allst[bi] for bi in range(nbatches)]
 
     NB = -(-max(S * GR, args.batches) // (S * GR)) * (S * GR)  # weak: whole groups on every stream
     plan = job_starts = None

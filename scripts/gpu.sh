@@ -57,6 +57,11 @@ run() {  # run NAME SECONDS CMD...: stdout+stderr to $OUT/NAME.log
     tail -3 "$OUT/$name.log"
     return $rc
 }
+shrink() {  # a profiler pass's output, small enough to come back (gpurun returns <= 64 MiB)
+    find "$1" -name "*kernel_trace.csv" -delete
+    find "$1" -name "*counter_collection.csv" -exec gzip -f {} \;
+    return 0
+}
 for step in "$@"; do
     case $step in
         suite) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
@@ -221,17 +226,21 @@ for step in "$@"; do
             run trace_one_stream 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace1" -o run --output-format csv -- \
                 python3 -u bench.py --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1
             run trace_default 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace2" -o run --output-format csv -- \
-                python3 -u bench.py --no-cpu || exit 1 ;;
+                python3 -u bench.py --no-cpu || exit 1
+            shrink "$OUT/trace1"; shrink "$OUT/trace2" ;;
         pmcw)  # the WRITE_SIZE pass alone (a pass that hangs can be re-run on its own)
             P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
             run pmc_write 170 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run \
-                --output-format csv -- python3 -u bench.py $P || exit 1 ;;
+                --output-format csv -- python3 -u bench.py $P || exit 1
+            shrink "$OUT/pmc_write" ;;
         pmcfe)  # the FETCH_SIZE and request-split passes
             P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
             run pmc_fetch 170 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \
                 --output-format csv -- python3 -u bench.py $P || exit 1
+            shrink "$OUT/pmc_fetch"
             run pmc_ea 170 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
-                --kernel-trace -d "$OUT/pmc_ea" -o run --output-format csv -- python3 -u bench.py $P || exit 1 ;;
+                --kernel-trace -d "$OUT/pmc_ea" -o run --output-format csv -- python3 -u bench.py $P || exit 1
+            shrink "$OUT/pmc_ea" ;;
         pmc)
             P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
             run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run \

@@ -7,10 +7,16 @@ printed, copied under profiles/ for the record:
          PREFIX_bench_pmc_{fetch,ea,write,tcc}.json     (the bench line of that pass)
 """
 import csv
+import gzip
 import json
 import os
 import sys
 from collections import defaultdict
+
+def open_csv(path):
+    """A pass's counter CSV, gzipped on the box when the raw files would not fit gpurun's 64 MiB return."""
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -24,12 +30,12 @@ def main():
         path = None
         for root, _, files in os.walk(os.path.join(g, f"pmc_{p}")):
             for f in files:
-                if f.endswith("counter_collection.csv"):
+                if f.endswith("counter_collection.csv") or f.endswith("counter_collection.csv.gz"):
                     path = os.path.join(root, f)
         if path is None:
             raise SystemExit(f"no counter_collection.csv for pass {p} under {g}")
         tot, disp = defaultdict(float), defaultdict(set)
-        for r in csv.DictReader(open(path)):
+        for r in csv.DictReader(open_csv(path)):
             k = (r["Kernel_Name"][:120], r["Counter_Name"])
             tot[k] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])

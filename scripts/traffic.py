@@ -18,10 +18,16 @@ launch's kernels (k_group_key x2, k_group_scan, k_search_grouped,
 k_group_tiles, k_emit — or k_search, k_emit), and for the search kernel
 alone."""
 import csv
+import gzip
 import json
 import os
 import sys
 from collections import defaultdict
+
+def open_csv(path):
+    """A pass's counter CSV, gzipped on the box when the raw files would not fit gpurun's 64 MiB return."""
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LAUNCH = ("k_search", "k_emit", "k_scan", "k_group_")
@@ -32,7 +38,7 @@ def sums(path):
     kernel alone, and the launch count (search-kernel dispatches)."""
     tot, srch = defaultdict(float), defaultdict(float)
     launches = set()
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(open_csv(path)):
         name = r["Kernel_Name"]
         if not any(k in name for k in LAUNCH):
             continue
@@ -52,7 +58,7 @@ def bench_json(log):
 def csv_of(d):
     for root, _, files in os.walk(d):
         for f in files:
-            if f.endswith("counter_collection.csv"):
+            if f.endswith("counter_collection.csv") or f.endswith("counter_collection.csv.gz"):
                 return os.path.join(root, f)
     raise SystemExit(f"no counter_collection.csv under {d}")
 
