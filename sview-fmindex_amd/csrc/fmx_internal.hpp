@@ -405,7 +405,18 @@ constexpr uint32_t kGroupPackBits = 96;
 constexpr uint32_t kGroupedXcd = 1;  // k_search_grouped opts: deal the key order out XCD by XCD
 constexpr uint32_t kWsortBytes = 1024 + 256 * 16;  // its in-workgroup sort's LDS (256 counters, 256 records)
 constexpr uint32_t kGroupRawStage = 216;  // raw records: patterns up to this long are staged in LDS by the search
-constexpr uint32_t kGroupCounterRoom = kGroupBins;
+// Each key's run of the sorted order is split into kGroupSlots sub-runs, one
+// per slot = chunk mod 8 — the XCD that places the chunk, under the
+// round-robin placement of workgroups (speed depends on it, correctness
+// does not): every chunk an XCD places writes its key-k patterns next to the
+// ones its other chunks wrote, so the scattered 16-B record writes fill whole
+// lines in that XCD's L2 before they leave it.  Counters key-major: key k,
+// slot s at k * kGroupSlots + s.
+#ifndef FMX_GROUP_SLOTS
+#define FMX_GROUP_SLOTS 8
+#endif
+constexpr uint32_t kGroupSlots = FMX_GROUP_SLOTS;
+constexpr uint32_t kGroupCounterRoom = kGroupBins * kGroupSlots;
 // Batches per grouped launch: up to kMaxMega, as several LocateGroups of at
 // most kMaxGroup (kernel arguments) whose key, place, tile and emit kernels run
 // per group and whose count scan, refine and search run once over the whole

@@ -626,12 +626,16 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     // global adds for all of them; measured no faster than one, r4w: the
     // atomics do not bound it), the place pass one
     constexpr uint32_t CPW = PLACE ? 1u : kCountChunks;
+    // the chunks' slot (kGroupSlots): the place pass's chunk is its workgroup; the count pass's
+    // workgroup w takes chunks of one slot, w mod S + S (CPW (w div S) + r), r < CPW
+    constexpr uint32_t S = kGroupSlots;
+    const uint32_t slot = blockIdx.x % S;
     uint32_t key_r[PPT], rank_r[PPT];
     U4 rec_r[PLACE ? PPT : 1];
     uint64_t pfirst = 0, pn = 0;  // (the place pass's one chunk, after the loop)
 #pragma unroll
     for (uint32_t r = 0; r < CPW; ++r) {
-    const uint32_t c = blockIdx.x * CPW + r;
+    const uint32_t c = PLACE ? blockIdx.x : (blockIdx.x / S) * (S * CPW) + r * S + slot;
     if constexpr (!PLACE) {
         const uint32_t nchunks = grp.chunk_begin[grp.n - 1] +
                                  (uint32_t)(((grp.b[grp.n - 1].npat + 255) / 256 + kGroupChunkTiles - 1) /
@@ -718,7 +722,7 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
 #pragma unroll
         for (uint32_t u = 0; u < per; ++u) {
             const uint32_t h = hist[u * T + t];
-            if (h) atomicAdd(grp.gcount + u * T + t, h);
+            if (h) atomicAdd(grp.gcount + (u * T + t) * S + slot, h);
         }
         return;
     } else {
@@ -727,7 +731,7 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
 #pragma unroll
         for (uint32_t u = 0; u < per; ++u) h[u] = hist[u * T + t];
 #pragma unroll
-        for (uint32_t u = 0; u < per; ++u) base[u] = h[u] ? atomicAdd(grp.gcount + u * T + t, h[u]) : 0u;
+        for (uint32_t u = 0; u < per; ++u) base[u] = h[u] ? atomicAdd(grp.gcount + (u * T + t) * S + slot, h[u]) : 0u;
 #pragma unroll
         for (uint32_t u = 0; u < per; ++u) hist[u * T + t] = base[u];  // the chunk's first position per key
         __syncthreads();
@@ -797,7 +801,8 @@ __global__ __launch_bounds__(1024) void k_group_refine(const QueryArgs a, const 
     }
     __syncthreads();
     for (uint32_t k = blockIdx.x; k < kGroupBins; k += gridDim.x) {
-    uint64_t end = grp.gcount[k], beg = k ? grp.gcount[k - 1] : 0;
+    // (key k's run: its slots' sub-runs, one after another)
+    uint64_t end = grp.gcount[k * kGroupSlots + kGroupSlots - 1], beg = k ? grp.gcount[k * kGroupSlots - 1] : 0;
     end = end < total ? end : total;
     beg = beg < end ? beg : end;
     if (end - beg < 2) continue;  // (workgroup-uniform)

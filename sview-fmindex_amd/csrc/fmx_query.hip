@@ -69,23 +69,28 @@ __global__ __launch_bounds__(256) void k_scan(const LocateGroup grp) {
 // ---------------------------------------------------------- grouped launches
 // (k_group_key<count / place> and k_search_grouped: fmx_kernels.hpp)
 
-// 2. The launch's key counts -> each key's first sorted position (exclusive
-// scan in place).
+// 2. The launch's key counts (per key and slot, key-major) -> each sub-run's
+// first sorted position (exclusive scan in place; 16 counters per thread per
+// pass, every load of a pass in flight at once).
 __global__ __launch_bounds__(256) void k_group_scan(uint32_t *cnt) {
     __shared__ uint64_t s_scan[4];
-    constexpr uint32_t per = kGroupBins / 256;
-    uint32_t v[per], sum = 0;
+    constexpr uint32_t per = 16;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < kGroupCounterRoom; base += 256 * per) {
+        uint32_t v[per], sum = 0;
 #pragma unroll
-    for (uint32_t u = 0; u < per; ++u) {
-        v[u] = cnt[threadIdx.x * per + u];
-        sum += v[u];
-    }
-    uint64_t tot;
-    uint32_t run = (uint32_t)block_excl_scan(sum, &tot, s_scan);
+        for (uint32_t u = 0; u < per; ++u) {
+            v[u] = cnt[base + threadIdx.x * per + u];
+            sum += v[u];
+        }
+        uint64_t tot;
+        uint32_t run = carry + (uint32_t)block_excl_scan(sum, &tot, s_scan);
 #pragma unroll
-    for (uint32_t u = 0; u < per; ++u) {
-        cnt[threadIdx.x * per + u] = run;
-        run += v[u];
+        for (uint32_t u = 0; u < per; ++u) {
+            cnt[base + threadIdx.x * per + u] = run;
+            run += v[u];
+        }
+        carry += (uint32_t)tot;
     }
 }
 
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(256) void k_group_check_order(const QueryArgs a, co
     __syncthreads();
     const uint64_t sp = (uint64_t)blockIdx.x * 256u + t, total = grp.gtotal;
     if (sp >= total) return;
-    bool bad = grp.gcount[kGroupBins - 1] != total;  // (the last run ends at the launch's end)
+    bool bad = grp.gcount[kGroupCounterRoom - 1] != total;  // (the last run ends at the launch's end)
     const uint32_t js = lds_upper(gt.first, grp.gn, sp);
     const U4 e = reinterpret_cast<const U4 *>(gt.desc[js].sorted)[sp - gt.first[js]];
     const uint32_t jb = lds_upper(gt.vfirst, grp.gn, e.w);
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(256) void k_group_check_order(const QueryArgs a, co
     uint32_t lo = 0, hi = kGroupBins - 1;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if ((uint64_t)grp.gcount[mid] > sp) hi = mid;
+        if ((uint64_t)grp.gcount[mid * kGroupSlots + kGroupSlots - 1] > sp) hi = mid;
         else lo = mid + 1;
     }
     const uint32_t m = B.stride;
@@ -487,7 +492,7 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
     // the key counters start at zero whatever an earlier launch on this
     // workspace did, and the table is in place: both ordered
     // before the count pass on the stream
-    hipError_t e = hipMemsetAsync(gcount, 0, 4ull * kGroupBins, stream);
+    hipError_t e = hipMemsetAsync(gcount, 0, 4ull * kGroupCounterRoom, stream);
     if (e != hipSuccess) return e;
     if ((e = put_bytes(d_tab->first, tab->first, 8ull * gn, stream)) != hipSuccess ||
         (e = put_bytes(d_tab->vfirst, tab->vfirst, 4ull * gn, stream)) != hipSuccess ||
@@ -499,7 +504,9 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
     for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t chunks = grps[g].chunk_begin[grps[g].n - 1] +
                                 (uint32_t)group_chunks(grps[g].b[grps[g].n - 1].npat);
-        hipLaunchKernelGGL((k_group_key<5, false, true>), dim3((chunks + kCountChunks - 1) / kCountChunks),
+        // (workgroups of kCountChunks chunks of one slot each: kGroupSlots per kGroupSlots x kCountChunks chunks)
+        const uint32_t span = kGroupSlots * kCountChunks;
+        hipLaunchKernelGGL((k_group_key<5, false, true>), dim3((chunks + span - 1) / span * kGroupSlots),
                            dim3(1024), 0, stream, qa, grps[g], rb);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -231,7 +231,9 @@ def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb
     check_simt(pkg, O, blob, pb, planes, vb, pats, 1)
 
 
-GROUP_BINS = 8192  # fmx_internal.hpp kGroupBins: the key counters' 32 KiB
+GROUP_BINS = 8192  # fmx_internal.hpp kGroupBins
+GROUP_SLOTS = 8  # kGroupSlots: key k's sub-run of slot s counts at k * 8 + s (the counters' 256 KiB)
+COUNTERS = GROUP_BINS * GROUP_SLOTS
 
 
 def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
@@ -260,12 +262,13 @@ def test_group_check_catches_dirty_counters(pkg, O, simt, monkeypatch):
     want = orc.locate_batch(data, offsets)
 
     def inject(words):
-        w = (C.c_uint32 * GROUP_BINS)(*words)
-        simt.simt_memset_fault(4 * GROUP_BINS, w, GROUP_BINS)
+        w = (C.c_uint32 * COUNTERS)(*words)
+        simt.simt_memset_fault(4 * COUNTERS, w, COUNTERS)
 
-    shifted = [0] * GROUP_BINS
-    shifted[1], shifted[2] = 0xFFFFFFFF, 1
-    over = [0] * GROUP_BINS
+    # (the one chunk is slot 0's)
+    shifted = [0] * COUNTERS
+    shifted[1 * GROUP_SLOTS], shifted[2 * GROUP_SLOTS] = 0xFFFFFFFF, 1
+    over = [0] * COUNTERS
     over[0] = 5
     for check, words, caught in (("1", shifted, True), ("0", shifted, False), ("0", over, True),
                                  ("1", over, True)):
