@@ -38,6 +38,8 @@
 #   chainab  C2 (grouped) ended by k_emit_chain vs k_group_tiles + k_emit (FMX_EMIT_CHAIN=0), alternating twice
 #   psweep   C2 at 100k / 200k / 400k patterns per batch (256 batches per launch: 25.6 / 51.2 / 102.4 M per launch)
 #   groupedtest  tests/test_gpu_grouped.py and tests/test_gpu_fused.py only
+#   slotab   C2 with the per-XCD sub-runs (8 slots) vs one run per key (sview-fmindex_amd/lib/ab/libfmx_s1.so),
+#            alternating twice, then a one-stream kernel trace of each
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   fusedab  the fused launch vs the two-kernel path (FMX_FUSED=0): single batch, C1, C4, alternating twice;
 #            then the single-batch kernel trace of the fused build
@@ -199,6 +201,19 @@ for step in "$@"; do
             done ;;
         groupedtest) run pytest_grouped 900 python -u -m pytest tests/test_gpu_grouped.py tests/test_gpu_fused.py -x -v \
                 --timeout 300 --timeout-method thread || exit 1 ;;
+        slotab)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "slots8_$r" 400 $B || exit 1
+                FMX_LIB=$PWD/sview-fmindex_amd/lib/ab/libfmx_s1.so run "slots1_$r" 400 $B || exit 1
+            done
+            run slots8_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/s8" -o run --output-format csv -- \
+                python3 -u bench.py --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1
+            shrink "$OUT/s8"
+            FMX_LIB=$PWD/sview-fmindex_amd/lib/ab/libfmx_s1.so run slots1_trace 400 rocprofv3 --kernel-trace --stats \
+                -d "$OUT/s1" -o run --output-format csv -- \
+                python3 -u bench.py --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1
+            shrink "$OUT/s1" ;;
         megab)
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
             for r in 1 2; do
