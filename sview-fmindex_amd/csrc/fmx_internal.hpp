@@ -405,15 +405,16 @@ constexpr uint32_t kGroupPackBits = 96;
 constexpr uint32_t kGroupedXcd = 1;  // k_search_grouped opts: deal the key order out XCD by XCD
 constexpr uint32_t kWsortBytes = 1024 + 256 * 16;  // its in-workgroup sort's LDS (256 counters, 256 records)
 constexpr uint32_t kGroupRawStage = 216;  // raw records: patterns up to this long are staged in LDS by the search
-// Each key's run of the sorted order is split into kGroupSlots sub-runs, one
-// per slot = chunk mod 8 — the XCD that places the chunk, under the
-// round-robin placement of workgroups (speed depends on it, correctness
-// does not): every chunk an XCD places writes its key-k patterns next to the
-// ones its other chunks wrote, so the scattered 16-B record writes fill whole
-// lines in that XCD's L2 before they leave it.  Counters key-major: key k,
-// slot s at k * kGroupSlots + s.
+// Build option (A/B): each key's run of the sorted order split into
+// kGroupSlots sub-runs, one per slot = chunk mod kGroupSlots (8: the XCD that
+// places the chunk, under the round-robin placement of workgroups), so that
+// an XCD's scattered 16-B record writes would fill whole lines in its L2.
+// Measured slower at 8 (C2: place 894 vs 566 us, count 229 vs 157 us per
+// group, 3.85 vs 4.01e9; profiles/r5/r5sab_*): the place pass is not bound
+// by partial-line writes.  Counters key-major: key k, slot s at
+// k * kGroupSlots + s.
 #ifndef FMX_GROUP_SLOTS
-#define FMX_GROUP_SLOTS 8
+#define FMX_GROUP_SLOTS 1
 #endif
 constexpr uint32_t kGroupSlots = FMX_GROUP_SLOTS;
 constexpr uint32_t kGroupCounterRoom = kGroupBins * kGroupSlots;

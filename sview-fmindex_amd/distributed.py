@@ -273,12 +273,12 @@ class ShardedLocate:
 
 def workspace_bytes(n: int, pos_bytes: int) -> int:
     """fmx_locate_workspace_size for n patterns (fmx_api.cpp ws_bytes_for):
-    [256 B + 4 x 8,192 x 8 key counters + a grouped launch's batch table (1,024
+    [256 B + 4 x 8,192 key counters + a grouped launch's batch table (1,024
     batches x 44 B)][tile counts and offsets: 2 x 8 B per 256-pattern
     tile][search records: 16 B (u32) / 24 B (u64) per pattern][16 B][sorted
     order: 16 B per pattern]."""
     tiles = max(1, -(-int(n) // 256))
-    return (256 + 4 * 8192 * 8 + GROUP_TAB_BYTES + 16 * tiles + int(n) * (16 if pos_bytes == 4 else 24) + 16
+    return (256 + 4 * 8192 + GROUP_TAB_BYTES + 16 * tiles + int(n) * (16 if pos_bytes == 4 else 24) + 16
             + 16 * int(n))
 
 

@@ -232,7 +232,7 @@ def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb
 
 
 GROUP_BINS = 8192  # fmx_internal.hpp kGroupBins
-GROUP_SLOTS = 8  # kGroupSlots: key k's sub-run of slot s counts at k * 8 + s (the counters' 256 KiB)
+GROUP_SLOTS = 1  # kGroupSlots (build option): key k's sub-run of slot s counts at k * GROUP_SLOTS + s
 COUNTERS = GROUP_BINS * GROUP_SLOTS
 
 
