@@ -401,7 +401,7 @@ static bool stream_capturing(hipStream_t s) {
 static hipError_t launch_emit(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp, uint32_t tiles,
                               uint32_t narrow, hipStream_t stream) {
     const Disp d = dispatch(ix);
-    uint32_t fold = 1;
+    uint32_t fold = ix->emit_fold ? 1u : 0u;
     for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
     if (!fold) {
         hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
