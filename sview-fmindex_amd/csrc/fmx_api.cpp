@@ -575,7 +575,7 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     // the fused launch (k_locate) and the bound on its waits: 4 s of the wall clock by default
     if (const char *e = getenv("FMX_FUSED")) ix->fused = e[0] != '0';
     if (const char *e = getenv("FMX_EMIT_CHAIN")) ix->emit_chain = e[0] != '0';
-    if (const char *e = getenv("FMX_EMIT_FOLD")) ix->emit_fold = e[0] != '0';
+    if (const char *e = getenv("FMX_EMIT_FOLD")) ix->emit_fold = e[0] != '0' ? 1 : 0;
     if (const char *e = getenv("FMX_FUSED_MAX_TILES")) ix->fused_max_tiles = strtoull(e, nullptr, 0);
     {
         uint64_t ms = 4000;

@@ -245,9 +245,9 @@ struct fmx_index {
     // as k_locate) instead of k_group_tiles + k_emit, when every batch has at most kFoldTiles tiles
     // (680 vs 235 us per C2 launch: the polls of ~2,000 short resident workgroups, profiles/r5/r5w_chain_*)
     bool emit_chain = false;
-    // k_emit sums the earlier tiles' counts itself for batches of at most kFoldTiles tiles (FMX_EMIT_FOLD=0:
-    // k_scan first for every batch, A/B)
-    bool emit_fold = true;
+    // k_emit sums the earlier tiles' counts itself for batches of at most kFoldTiles tiles in launch order;
+    // grouped launches run k_scan first (-1: that policy; FMX_EMIT_FOLD=1 / 0: fold / k_scan everywhere)
+    int emit_fold = -1;
     mutable std::atomic<uint64_t> launches_chained{0};  // (a subset of the grouped launches)
     std::mutex status_mu;
     uint8_t *d_dlut = nullptr;

@@ -401,7 +401,9 @@ static bool stream_capturing(hipStream_t s) {
 static hipError_t launch_emit(const fmx_index *ix, const QueryArgs &qa, const LocateGroup &grp, uint32_t tiles,
                               uint32_t narrow, hipStream_t stream) {
     const Disp d = dispatch(ix);
-    uint32_t fold = ix->emit_fold ? 1u : 0u;
+    // (a grouped launch's batches get k_scan: 885-895 vs 923-939 us per 102.4 M-pattern launch with
+    // k_emit's own sums, profiles/r5/r5fold_*; FMX_EMIT_FOLD=1 / 0 forces either)
+    uint32_t fold = (ix->emit_fold == 1 || (ix->emit_fold < 0 && !narrow)) ? 1u : 0u;
     for (uint32_t j = 0; j < grp.n; ++j) fold &= (grp.b[j].npat + 255) / 256 <= kFoldTiles ? 1u : 0u;
     if (!fold) {
         hipLaunchKernelGGL(k_scan, dim3(grp.n), dim3(256), 0, stream, grp);
