@@ -95,11 +95,12 @@ CONFIGS = {
     "c3": dict(text_len=1_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=4, planes=3, vec=64, k=3, sr=2,
                patterns=100_000, m=20, total=10_000_000, group=256,
                desc="C3: 1 Gbp ACGT, 10,000,000 x 20 bp sharded over the GPUs, u32/Block3<u64>, sr 2, k 3"),
-    # configs[3]: large-alphabet occ path.  256 batches per launch in launch order (3.59 vs 3.27e9 at 8 per
-    # launch; grouped launches measured slower: 3.29e9 keyed on the last 3 residues, 3.17e9 with the refine
-    # pass — the presort upper bound 4.49e9 is eaten by the permutation's scattered writes; profiles/r5/r5f_*)
+    # configs[3]: large-alphabet occ path.  1,024 batches per launch, grouped (the engine's default from
+    # 2^26 patterns for a 3-residue key): 3.68e9 vs 3.42-3.45 in launch order at 256 or 1,024 per launch
+    # (profiles/r5/r5c4m_*); at 256 per launch grouping lost (3.29 vs 3.59e9, r5f_*: the permutation's
+    # scattered writes cost more than 25.6 M patterns share)
     "c4": dict(text_len=1_000_000_000, alphabet=AMINO, symbols=[bytes([c, c + 32]) for c in AMINO] + [b"Xx"],
-               pos=4, planes=5, vec=64, k=3, sr=2, patterns=100_000, m=12, total=0, group=256,
+               pos=4, planes=5, vec=64, k=3, sr=2, patterns=100_000, m=12, total=0, group=1024,
                desc="C4: 1 G-residue protein text (20 aa + X wildcard), 100,000 x 12 aa, u32/Block5<u64>, sr 2, k 3"),
     # configs[4]: long patterns, wide blocks, u64 positions (1 M patterns over the GPUs)
     "c5": dict(text_len=3_000_000_000, alphabet=b"ACGT", symbols=ACGTN, pos=8, planes=3, vec=128, k=3, sr=2,

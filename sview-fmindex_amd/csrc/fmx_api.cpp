@@ -659,14 +659,16 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (S >= 2)
         for (uint64_t bins = S; bins <= kGroupBins && ix->gkey_len < 16; bins *= S) ++ix->gkey_len;
     // on by default for launches of at least 2^20 patterns whose key spans at
-    // least 5 symbols (DNA: 6; a 20-residue alphabet keys on 3, no more than
-    // its k-mer seed, and loses: DESIGN.md §5).  Below ~1 M patterns the
-    // dealing out's fixed cost eats the sharing: at 256 batches of 1,000 (C1)
-    // launch order runs 8.0 vs 4.2 x 10^9 grouped (profiles/r5/r5p_*, r5q_*),
-    // at 0.8 M patterns on 1 Gbp the two were equal and at 1.6 M grouping
-    // gained 6 % (round 3); at 25.6 M patterns it gains 4 % on a 4 Mbp text
-    // and 50 % from 16 Mbp up (r5q_size_*, r5r_size_*).
-    ix->grouped_min = ix->gkey_len >= 5 ? (1ull << 20) : ~0ull;
+    // least 5 symbols (DNA: 6), and of at least 2^26 whose key is shorter (a
+    // 20-residue alphabet keys on 3, no more than its k-mer seed: at 25.6 M
+    // patterns per launch grouping lost, 3.29 vs 3.59 x 10^9, profiles/r5/
+    // r5f_*; at 102.4 M it won, 3.68 vs 3.42-3.45, r5c4m_*).  Below ~1 M
+    // patterns the dealing out's fixed cost eats the sharing: at 256 batches
+    // of 1,000 (C1) launch order runs 8.0 vs 4.2 x 10^9 grouped (r5p_*,
+    // r5q_*), at 0.8 M patterns on 1 Gbp the two were equal and at 1.6 M
+    // grouping gained 6 % (round 3); at 25.6 M patterns it gains 4 % on a
+    // 4 Mbp text and 50 % from 16 Mbp up (r5q_size_*, r5r_size_*).
+    ix->grouped_min = ix->gkey_len >= 5 ? (1ull << 20) : (1ull << 26);
     if (const char *e = getenv("FMX_GROUPED")) {
         if (e[0] == '0') ix->grouped_min = ~0ull;
         else if (e[0] == '1') ix->grouped_min = 1;

@@ -180,10 +180,11 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
 
 
 def test_default_policy_by_alphabet(pkg, O, monkeypatch):
-    """Grouping is on by default (launches of at least 2^20 patterns) where
-    the key spans at least 5 symbols (ACGT: 6) and off for a 20-residue
-    alphabet (key of 3 symbols: no LF step beyond a k = 3 seed shared by the
-    key alone)."""
+    """Grouping is on by default for launches of at least 2^20 patterns where
+    the key spans at least 5 symbols (ACGT: 6), and from 2^26 for a
+    20-residue alphabet (key of 3 symbols: no LF step beyond a k = 3 seed
+    shared by the key alone — only a launch of ~100 M patterns shares
+    enough deeper steps to pay for the dealing out)."""
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
     rng = np.random.default_rng(9)
@@ -194,7 +195,7 @@ def test_default_policy_by_alphabet(pkg, O, monkeypatch):
         ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block5(pkg.Vector.U64), options=1)
         info = ix.info()
         assert info["group_key_len"] == want_len and info["group_key_base"] == len(chars)
-        assert (info["grouped_min"] == 1 << 20) == on
+        assert info["grouped_min"] == (1 << 20 if on else 1 << 26)
         ix.close()
 
 
