@@ -347,7 +347,7 @@ def test_hbm_per_rank_world8(pkg, cfg):
     hbm = D.hbm_per_rank(blob=blob, records=records, text=c["text_len"], batch_sizes=sizes, m=m, pos_bytes=P,
                          world=world, group=GR, loc_cap=[b + b // 8 + 4096 for b in sizes], gather=True)
     assert hbm["total"] == sum(v for k, v in hbm.items() if k != "total")
-    assert hbm["total"] < 0.25 * 288e9, hbm  # (c2: ~40 GB, c5: ~21 GB)
+    assert hbm["total"] < 0.25 * 288e9, hbm  # (c2: ~37.5 GB, c5: ~21 GB)
     if cfg == "c2":
         # two launch groups of 102.4 M patterns: each rank's part ~0.9 GB with room, gathered x8
         assert 12e9 < hbm["gather_slabs"] < 20e9, hbm
