@@ -360,10 +360,13 @@ hipError_t launch_locate_groups(const fmx_index *ix, LocateGroup *grps, uint32_t
 // k_emit sums the earlier tiles' counts itself for batches of at most this
 // many tiles; larger ones get their tile offsets from k_scan first.
 constexpr uint64_t kFoldTiles = 2048;
-// k_locate (the fused launch) only for patterns up to this long: a tile's
-// search, which later tiles of its batch wait for, stays far below the wait
-// bound (fmx_index::fused_late_ticks).
-constexpr uint32_t kFusedMaxLen = 4096;
+// k_locate (the fused launch) only for patterns up to this long: it gains
+// where a tile's search is short (20 bp: one 100k batch 64.0 vs 66.7 us, C1
+// +12 %, profiles/r5/r5t_*) and loses where it is long (C5's 150 bp: 3.25
+// vs 3.33 x 10^9 — workgroups that finish early hold their slots while they
+// wait for their batch's slower tiles, r5c5f_*); it also keeps every wait far
+// below its bound (fmx_index::fused_late_ticks).
+constexpr uint32_t kFusedMaxLen = 64;
 // k_group_tiles takes this many tiles of one batch per workgroup: each of its
 // waves has that many record loads in flight instead of one (a workgroup's
 // life is mostly one HBM round trip; 121 -> 64 us per C2 launch at 4,
