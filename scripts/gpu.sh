@@ -39,6 +39,7 @@
 #   psweep   C2 at 100k / 200k / 400k patterns per batch (256 batches per launch: 25.6 / 51.2 / 102.4 M per launch)
 #   groupedtest  tests/test_gpu_grouped.py and tests/test_gpu_fused.py only
 #   c4mega   C4 at 1,024 batches per launch: launch order vs grouped (and + refine), and launch order at 256
+#   c4ab     C4 at 1,024 per launch: grouped (default) vs launch order, alternating twice
 #   streamab C2 on 2 vs 3 streams at 1,024 batches per launch, alternating twice
 #   foldab   C2: k_emit's own tile sums vs k_scan first (FMX_EMIT_FOLD=0), and the refine pass, alternating twice
 #   slotab   C2 with the per-XCD sub-runs (8 slots) vs one run per key (sview-fmindex_amd/lib/ab/libfmx_s1.so),
@@ -219,10 +220,16 @@ for step in "$@"; do
             shrink "$OUT/s1" ;;
         c4mega)  # C4 at 1,024 batches per launch: launch order vs grouped (keyed on 3 residues; + refine)
             B="python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch"
-            run c4_lo_g256 400 $B || exit 1
-            run c4_lo_g1024 400 $B --group 1024 || exit 1
+            FMX_GROUPED=0 run c4_lo_g256 400 $B --group 256 || exit 1
+            FMX_GROUPED=0 run c4_lo_g1024 400 $B --group 1024 || exit 1
             FMX_GROUPED=1 run c4_grouped_g1024 400 $B --group 1024 || exit 1
             FMX_GROUPED=1 FMX_GROUP_REFINE_MIN=1 run c4_refine_g1024 400 $B --group 1024 || exit 1 ;;
+        c4ab)  # C4 at 1,024 per launch: grouped (the default) vs launch order (FMX_GROUPED=0), alternating twice
+            B="python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "c4_grouped_$r" 400 $B || exit 1
+                FMX_GROUPED=0 run "c4_order_$r" 400 $B || exit 1
+            done ;;
         streamab)  # C2 on 2 vs 3 streams (1,024 batches per launch), alternating twice
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
             for r in 1 2; do
