@@ -557,7 +557,7 @@ def main():
     total = args.total_patterns if args.total_patterns >= 0 else cfg["total"]
     P = cfg["pos"]
     S = max(1, args.streams or cfg.get("streams", 2))
-    GR = max(1, min(args.group or cfg.get("group", 8), 1024))
+    GR = max(1, min(args.group or cfg.get("group", 8), 2048))
     BLK = cfg["planes"] * cfg["vec"] // 8
     position = pkg.u32 if P == 4 else pkg.u64
     block = getattr(pkg.blocks, f"Block{cfg['planes']}")(pkg.Vector(cfg["vec"]))
