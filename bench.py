@@ -19,10 +19,13 @@ K-mer table, full SA, text: ~147 GB of HBM at C2), outside SURVEY §8.
 
 One step = one full count+locate pass over one batch: k-mer seed + LF loop
 for every pattern, the walk of every occurrence row, output offsets and all
-locations written to that batch's own HBM outputs.  Up to 8 steps' batches
-share one kernel launch (fmx_locate_group_async) and launches alternate over
-two streams; 32 distinct batches are cycled so that no pass finds the
-previous pass's index lines in cache.  Inputs (text, blob, index, patterns)
+locations written to that batch's own HBM outputs.  Many steps' batches
+share one kernel launch (fmx_locate_group_async; `--group`, at most 2,048):
+C2 and C4 1,024 per (grouped) launch, C1 and C3 256, C5 8.  Launches
+alternate over two streams, each stream with its own launch group of
+distinct batches (C2: 2,048 distinct batches, ~20 GB of patterns and
+outputs), so that no pass finds the previous pass's index lines in cache.
+Inputs (text, blob, index, patterns)
 are resident in HBM before the timed region.  The K steps are timed as a
 whole and repeated until the timed region lasts at least --min-seconds
 (0.2 s): a few-hundred-microsecond region is noise.
@@ -151,13 +154,18 @@ def parse():
                     help="skip the single_batch leg (one 100k batch per fmx_locate_batch_async call)")
     ap.add_argument("--single-batch-only", action="store_true",
                     help="run only the headline setup and the single_batch leg (no other legs)")
-    ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2, c1: 8)")
+    ap.add_argument("--streams", type=int, default=None, help="launches in flight (HIP streams; default 2)")
     ap.add_argument("--batches", type=int, default=32,
                     help="distinct batches cycled (weak-scaling configs; at least one launch group per stream)")
-    ap.add_argument("--group", type=int, default=None, help="batches per launch (at most 1024; fmx_locate_group_async; default 8; c1, c2, c3, c4: 256)")
+    ap.add_argument("--group", type=int, default=None, help="batches per launch (at most 2,048; fmx_locate_group_async; c2, c4: 1,024; c1, c3: 256; c5: 8)")
     ap.add_argument("--graph", action="store_true",
                     help="capture one pass (every launch, forked over the streams) in a HIP graph and replay it: "
                          "one host call per pass instead of one per launch (launch-bound configs)")
+    ap.add_argument("--gather", choices=("all", "counts"), default="all",
+                    help="N > 1 (and FMX_BENCH_DIST=1): what each launch group's in-step all-gather moves — all: "
+                         "counts and locations (north_star's single all-gather, default); counts: the count slabs "
+                         "alone (the job's offsets on every rank), the locations gathered once after the timed "
+                         "region")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment (weak configs): each launch group's patterns arranged so that workgroup "
@@ -712,7 +720,7 @@ def main():
             ev.record(grp["stream"])
             comm.wait_event(ev)
             with torch.cuda.stream(comm):
-                works.append(jg.gather(gi, async_op=True))
+                works.append(jg.gather(gi, async_op=True, part=args.gather))
                 done = torch.cuda.Event()
                 done.record(comm)
                 gathered[gi] = done
@@ -733,11 +741,24 @@ def main():
         value = int(pt2.item()) / e2
         if gather is None:
             gather = {}
+        # what each policy moves per pass and the xGMI rate per GPU it needs to
+        # hide behind the compute (bytes every rank receives / the compute-only
+        # time of a pass), at this N and, for the same per-rank shape, at N = 8
+        pass_s = elapsed / max(passes, 1)
+        per_rank_slab = {pol: jg.bytes_per_pass(pol) / max(world, 1) for pol in ("all", "counts")}
         gather.update({"inside_timed_step": True, "value_compute_only": value_compute,
-                       "collectives_per_launch": 1,
-                       "bytes_gathered_per_pass": jg.bytes_per_pass(),
+                       "policy": args.gather, "collectives_per_launch": 1,
+                       "bytes_gathered_per_pass": jg.bytes_per_pass(args.gather),
+                       "bytes_per_pass": {pol: jg.bytes_per_pass(pol) for pol in ("all", "counts")},
+                       "required_gbs_per_gpu": {pol: jg.bytes_per_pass(pol) / pass_s / 1e9
+                                                for pol in ("all", "counts")},
+                       "required_gbs_per_gpu_at_n8": {pol: 8 * per_rank_slab[pol] / pass_s / 1e9
+                                                      for pol in ("all", "counts")} if not strong else None,
                        "result_bytes_per_pass": jg.result_bytes(),
                        "gathered_over_result": jg.bytes_per_pass() / max(jg.result_bytes(), 1)})
+        if args.gather == "counts":
+            jg.gather_all()  # the locations once, after the timed region (assemble below)
+            torch.cuda.synchronize()
     if jg is not None:
         # the job's flat (offsets, locations) on the device; this rank's part
         # must equal what its own launches wrote
@@ -923,16 +944,20 @@ def main():
     # ---- one batch per call (the config's own batch, N = 1) ------------------
     if rank == 0 and world == 1 and not strong and not args.no_single_batch:
         result["single_batch"] = single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, args.seed,
-                                                  min(args.min_seconds, 1.0), pdt_t, P)
+                                                  min(args.min_seconds, 1.0), pdt_t, P, GR, S)
     if args.single_batch_only:
         args.no_blob_layout = args.no_cpu = True
         args.derived = False
 
     # ---- the blob's own layout (options 0, N = 1) -----------------------------
-    # the GPU's answers for the CPU leg to check (up to 32 batches, host copies)
-    host_batches = []
+    # the GPU's answers for the CPU leg to check (32 batches spread evenly over
+    # the workload's distinct batches — at C2's 2,048: every 66th, so every
+    # kernel-argument group of 256 of both grouped launches is sampled; host copies)
+    host_batches, host_idx, n_distinct = [], [], len(w.batches)
     if rank == 0 and world == 1 and not args.no_cpu:
-        for bt in w.batches[:32]:
+        host_idx = sorted({int(round(x)) for x in np.linspace(0, n_distinct - 1, min(32, n_distinct))})
+        for bi in host_idx:
+            bt = w.batches[bi]
             bo = bt["loff"].cpu().numpy().view(np.uint64).copy()
             host_batches.append((bt["pat"].cpu().numpy(), bt["n"], bo,
                                  bt["locs"][:int(bo[-1])].cpu().numpy().view(pdt_np).copy()))
@@ -1022,9 +1047,14 @@ def main():
             "value_1_thread": legs[1][0], "cores_source": src, "cpu_model": model,
             "host_cpus_visible": os.cpu_count(),
         }
+        idx_checked = [host_idx[i] for i in sorted(checked)]
+        groups = sorted({bi // 256 for bi in idx_checked})
         result.setdefault("parity", {"bit_exact_vs_cpu": exact, "patterns": nck, "batches": len(checked),
-                                     "scope": f"{len(checked)} of the workload's batches, every count and location"})
-        result["parity_cpu_leg"] = {"bit_exact": exact, "batches": len(checked), "patterns": nck}
+                                     "scope": f"{len(checked)} of the workload's {n_distinct} batches, spread "
+                                              f"over its kernel-argument groups of 256 {groups}, every count and "
+                                              f"location", "batch_indices": idx_checked})
+        result["parity_cpu_leg"] = {"bit_exact": exact, "batches": len(checked), "patterns": nck,
+                                    "batch_indices": idx_checked}
         result["speedup_vs_cpu"] = value / legs[threads][0]
         result["speedup_vs_cpu_1_thread"] = value / legs[1][0]
         if not exact:
@@ -1039,7 +1069,7 @@ def main():
         dist.destroy_process_group()
 
 
-def single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, seed, min_seconds, pdt_t, P):
+def single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, seed, min_seconds, pdt_t, P, GR, S):
     """BASELINE configs[1] as a caller of the reference's per-batch loop gets
     it (bench/src/locate/sview_memory.rs:32: one batch of 100,000 patterns per
     call): one fmx_locate_batch_async call per batch on one stream, calls back
@@ -1047,8 +1077,8 @@ def single_batch_leg(torch, ix, load, d_text, n, m, B, fixed, dev, seed, min_sec
     >= min_seconds — in launch order (FMX_GROUPED=0) and grouped
     (FMX_GROUPED=1: the batch dealt out by its last symbols on its own), each
     on an index of its own (the policy is read at load)."""
-    out = {"what": "one 100k-pattern batch per fmx_locate_batch_async call, one stream, calls back to back; "
-                   "the headline instead runs 256 batches per grouped launch (fmx_locate_group_async) on 2 streams"}
+    out = {"what": f"one {B:,}-pattern batch per fmx_locate_batch_async call, one stream, calls back to back; "
+                   f"the headline instead runs {GR:,} batches per launch (fmx_locate_group_async) on {S} streams"}
     stage_kb = min(56, -(-256 * m // 1024))
     for mode, name in (("0", "launch_order"), ("1", "grouped")):
         saved = os.environ.get("FMX_GROUPED")

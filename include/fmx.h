@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FMX_ABI_VERSION 7u
+#define FMX_ABI_VERSION 8u
 
 typedef enum fmx_status {
     FMX_OK = 0,
@@ -258,11 +258,18 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
  * the device before its search — a violation is FMX_E_DEVICE; debug).  One
  * kernel makes workgroups wait on others: the fused launch in launch order
  * (k_locate, fmx_index_info.launches_fused; FMX_FUSED=0 never) — a workgroup
- * waits for the lower-indexed workgroups of its batch, which the dispatcher
- * started before it; bounded (FMX_FUSED_TIMEOUT_MS, default 4 s, then
- * FMX_E_DEVICE).  The key counters and the batch table of a grouped launch
- * are in its first batch's workspace. */
+ * answers the tile of its ticket (the number of its batch's workgroups that
+ * started before it) and waits only for the earlier tiles of its batch, whose
+ * workgroups are therefore already running; bounded (FMX_FUSED_TIMEOUT_MS,
+ * default 4 s, then FMX_E_DEVICE).  The key counters and the batch table of a
+ * grouped launch are in its first batch's workspace. */
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n_patterns, uint64_t *bytes);
+
+/* The same size without an index (ABI 8): for n_patterns patterns of an
+ * index with pos_bytes-wide positions (4 or 8; FMX_E_ARG otherwise) — what a
+ * caller sizing HBM before it loads an index (e.g. the per-rank accounting of
+ * a sharded job) needs.  Equal to fmx_locate_workspace_size on such an index. */
+fmx_status fmx_workspace_bytes(uint64_t n_patterns, uint32_t pos_bytes, uint64_t *bytes);
 
 /* d_loc_offsets has n_patterns+1 entries; d_counts (optional, may be NULL)
  * receives P-wide counts; d_needed (device uint64) receives the total. */

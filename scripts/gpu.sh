@@ -45,6 +45,9 @@
 #   slotab   C2 with the per-XCD sub-runs (8 slots) vs one run per key (sview-fmindex_amd/lib/ab/libfmx_s1.so),
 #            alternating twice, then a one-stream kernel trace of each
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
+#   megatest test_gpu_mega.py (1,024-batch grouped launch, two-stream fused launches), test_gpu_fused.py,
+#            test_gpu_provenance.py
+#   ticketab the fused launch's tickets vs workgroup index order: single batch and C1, alternating twice
 #   fusedab  the fused launch vs the two-kernel path (FMX_FUSED=0): single batch, C1, C4, alternating twice;
 #            then the single-batch kernel trace of the fused build
 # Every step has its own time limit; the first failing step ends the run.
@@ -308,6 +311,18 @@ for step in "$@"; do
                 $CLI locate -d $D -a sview-memory --drop-caches && $CLI locate -d $D -a sview-mmap --drop-caches && \
                 $CLI locate -d $D -a sview-mmap --drop-caches --direct && md5sum $D/*-results.txt" || exit 1
             rm -rf "$D" ;;
+        megatest)  # round 6: the 1,024-batch grouped launch and the two-stream fused launches vs the oracle,
+            # the fused file, full-size blob provenance (GPU builder vs the oracle builder's SHA-256)
+            run pytest_mega 900 python -u -m pytest tests/test_gpu_mega.py tests/test_gpu_fused.py \
+                tests/test_gpu_provenance.py -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+        ticketab)  # the fused launch's per-batch tickets (default) vs workgroup index order (FMX_FUSED_TICKETS=0):
+            # single batch and C1 (fused launches), alternating twice
+            for r in 1 2; do
+                run "single_tk_$r" 300 python -u bench.py --single-batch-only || exit 1
+                FMX_FUSED_TICKETS=0 run "single_idx_$r" 300 python -u bench.py --single-batch-only || exit 1
+                run "c1_tk_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
+                FMX_FUSED_TICKETS=0 run "c1_idx_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

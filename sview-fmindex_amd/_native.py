@@ -91,6 +91,7 @@ SIGNATURES = {
     "fmx_locate_batch": (_i, [_p, _p, _p, _u64, _u32, _p, _p, _u64, _PU64]),
     "fmx_count_batch_async": (_i, [_p, _p, _p, _u64, _u32, _p, _p]),
     "fmx_locate_workspace_size": (_i, [_p, _u64, _PU64]),
+    "fmx_workspace_bytes": (_i, [_u64, _u32, _PU64]),
     "fmx_locate_batch_async": (_i, [_p, _p, _p, _u64, _u32, _p, _p, _p, _u64, _p, _p, _u64, _p]),
     "fmx_locate_jobs_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64]),
     "fmx_locate_group_async": (_i, [_p, C.POINTER(fmx_locate_job), _u64, _p]),

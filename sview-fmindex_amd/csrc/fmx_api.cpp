@@ -357,7 +357,8 @@ static int status_slot_locked(fmx_index *ix, hipStream_t s, bool launch) {
         ix->status_of.erase(ix->slots[idx].key);
     }
     StatusSlot &sl = ix->slots[idx];
-    if (hipMemsetAsync(ix->d_status + idx, 0, 4, s) != hipSuccess) {
+    if (hipMemsetAsync(ix->d_status + idx, 0, 4, s) != hipSuccess ||
+        hipMemsetAsync(ix->d_tickets + (uint64_t)idx * kMaxGroup, 0, 4ull * kMaxGroup, s) != hipSuccess) {
         sl.key = nullptr;
         ix->free_slots.push_back((uint32_t)idx);
         return -1;
@@ -569,6 +570,17 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     if (!ix->stream && hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) return FMX_E_DEVICE;
     if (hipMalloc(&ix->d_status, kStatusSlots * 4) != hipSuccess) return FMX_E_DEVICE;
     if (hipMemsetAsync(ix->d_status, 0, kStatusSlots * 4, ix->stream) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMalloc(&ix->d_tickets, 4ull * kStatusSlots * kMaxGroup) != hipSuccess) return FMX_E_DEVICE;
+    if (hipMemsetAsync(ix->d_tickets, 0, 4ull * kStatusSlots * kMaxGroup, ix->stream) != hipSuccess)
+        return FMX_E_DEVICE;
+    // each slot's status word is read back into a pinned word of its own (read_status)
+    if (hipHostMalloc(&ix->h_status, kStatusSlots * 4, hipHostMallocDefault) != hipSuccess) {
+        ix->h_status = nullptr;
+        return FMX_E_DEVICE;
+    }
+    ix->slot_mu.reset(new (std::nothrow) std::mutex[kStatusSlots]);
+    if (!ix->slot_mu) return FMX_E_DEVICE;
+    if (const char *e = getenv("FMX_FUSED_TICKETS")) ix->fused_tickets = e[0] != '0';
     if (hipStreamSynchronize(ix->stream) != hipSuccess) return FMX_E_DEVICE;
     ix->slots.assign(kStatusSlots, StatusSlot{});
     if (const char *e = getenv("FMX_SEARCH_PERSISTENT")) ix->search_persistent = e[0] == '1';
@@ -770,12 +782,26 @@ static fmx_status read_status(fmx_index *ix, hipStream_t s) {
     if (idx < 0) return dev_err(hipStreamSynchronize(s));  // never launched on: nothing latched
     uint32_t *w = ix->d_status + idx;
     uint32_t st = 0;
-    // (through the pinned stage: no DMA into this stack word; d2h returns
-    // once the word is here, so every launch queued on s before has finished)
-    if (ix->stage.d2h(&st, w, 4, s) != hipSuccess) return FMX_E_DEVICE;
+    {
+        // into the slot's own pinned word (no DMA into pageable memory), waiting on s alone: no lock
+        // that another stream's call needs is held across the wait (ADVICE r5 — the shared Stage was);
+        // the word is readable once s has drained, so every launch queued on s before has finished
+        std::lock_guard<std::mutex> g(ix->slot_mu[idx]);
+        volatile uint32_t *h = ix->h_status + idx;
+        *h = 0;
+        if (hipMemcpyAsync((void *)h, w, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return FMX_E_DEVICE;
+        st = *h;
+    }
     if (st) {
-        // ordered on s after every launch that could have set it: nothing is lost
-        if (hipMemsetAsync(w, 0, 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) return FMX_E_DEVICE;
+        // ordered on s after every launch that could have set it: nothing is lost; a late fused
+        // launch may have left its ticket counters off zero (claim_tile): they are zeroed too
+        if (hipMemsetAsync(w, 0, 4, s) != hipSuccess ||
+            ((st & kStatusLate) &&
+             hipMemsetAsync(ix->d_tickets + (uint64_t)idx * kMaxGroup, 0, 4ull * kMaxGroup, s) != hipSuccess) ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return FMX_E_DEVICE;
     }
     if (st & kStatusEmpty) return FMX_E_EMPTY_PATTERN;
     if (st & kStatusSymbol) return FMX_E_SYMBOL;
@@ -1073,6 +1099,8 @@ void fmx_free(fmx_index *ix) {
     if (ix->d_text) hipFree(ix->d_text);
     if (ix->d_tab) hipFree(ix->d_tab);
     if (ix->d_status) hipFree(ix->d_status);
+    if (ix->d_tickets) hipFree(ix->d_tickets);
+    if (ix->h_status) hipHostFree(ix->h_status);
     if (ix->d_blob_owned) hipFree(ix->d_blob_owned);
     if (ix->stream) hipStreamDestroy(ix->stream);
     delete ix;
@@ -1131,13 +1159,20 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
 // Locate workspace (fmx_internal.hpp, kWsHeader): [256 B reserved][group
 // key counters][tile counts: G][tile offsets: G][search records: n x
 // locate_rec_bytes(P)][to 16 B][sorted order: n x 16 B], G = ceil(n / 256).
-static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) {
-    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(ix->bv.L.pos_bytes) + 16 + 16 * n;
+static uint64_t ws_bytes_of(uint64_t n, uint32_t pos_bytes) {
+    return kWsHeader + 2 * locate_tiles_cap(n) * 8 + n * locate_rec_bytes(pos_bytes) + 16 + 16 * n;
 }
+static uint64_t ws_bytes_for(const fmx_index *ix, uint64_t n) { return ws_bytes_of(n, ix->bv.L.pos_bytes); }
 
 fmx_status fmx_locate_workspace_size(fmx_index *ix, uint64_t n, uint64_t *bytes) {
     if (!ix || !bytes) return FMX_E_ARG;
     *bytes = ws_bytes_for(ix, n);
+    return FMX_OK;
+}
+
+fmx_status fmx_workspace_bytes(uint64_t n, uint32_t pos_bytes, uint64_t *bytes) {
+    if (!bytes || (pos_bytes != 4 && pos_bytes != 8)) return FMX_E_ARG;
+    *bytes = ws_bytes_of(n, pos_bytes);
     return FMX_OK;
 }
 

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -203,6 +204,12 @@ struct fmx_index {
     uint32_t occ_mode = FMX_OCC_BLOB;
     uint32_t rec_bytes = 0;
     uint32_t *d_status = nullptr;  // kStatusSlots words: one per stream launched on
+    // per status slot, kMaxGroup ticket counters for the fused launches on its stream (take_ticket:
+    // zero between launches); FMX_FUSED_TICKETS=0 (A/B): workgroup index order instead
+    uint32_t *d_tickets = nullptr;
+    bool fused_tickets = true;
+    uint32_t *h_status = nullptr;               // pinned: kStatusSlots words (read_status)
+    std::unique_ptr<std::mutex[]> slot_mu;      // one per status slot (read_status)
     std::vector<fmx::StatusSlot> slots;                   // kStatusSlots
     std::unordered_map<const void *, uint32_t> status_of;  // stream -> slot
     std::vector<uint32_t> free_slots;
@@ -335,6 +342,9 @@ struct LocateGroup {
     // workgroups take tiles from this counter (batch 0's workspace header,
     // zero between launches: k_emit resets it); null = one workgroup per tile
     uint32_t *tile_ctr;
+    // k_locate / k_emit_chain: one ticket counter per batch (fmx_index::d_tickets, the launch's status
+    // slot's kMaxGroup words; take_ticket); null = each workgroup answers the tile of its own index
+    uint32_t *tickets;
 };
 // A LocateGroup ready to be filled: no batches, launch-order fields clear.
 // (Not zeroed as a whole: 25 KB per launch of host memset, and the kernels
@@ -347,6 +357,7 @@ inline void group_reset(LocateGroup &g) {
     g.gtab = nullptr;
     g.gn = g.vbase = 0;
     g.tile_ctr = nullptr;
+    g.tickets = nullptr;
 }
 // `mid` (optional): an event recorded between k_search and k_emit (timing).
 // Fills grp's per-launch fields (first, emit_begin, the grouped fields) in place.

@@ -425,13 +425,17 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_search_
 // output offsets and locations (emit_locations, as k_emit) — no search
 // records, no second kernel (a lone 100k batch: k_search 55.6 + k_emit
 // 13.3 us, profiles/r5/r5i_*).  Unlike every other kernel here, a workgroup
-// waits on others: on the workgroups of lower index in its own batch, which
-// the dispatcher has started before it (workgroups are dispatched in index
-// order, MI355X_MICROARCH.md § dispatch), so the wait always ends; it is
-// bounded all the same (late_ticks of the 100 MHz wall clock, then
-// kStatusLate: FMX_E_DEVICE, never a hang), and only launches whose patterns
-// are short enough that a tile's search is bounded take this path
-// (fmx_query.hip, launch_split).
+// waits on others: on the earlier tiles of its own batch.  Which tile a
+// workgroup answers is its TICKET (take_ticket: the number of the batch's
+// workgroups that started before it, as rocPRIM's ordered block id), not its
+// index: the XCDs dispatch a launch's workgroups independently, and beside
+// another stream's launch a lower-index workgroup could wait for a slot held
+// by waiters.  A ticket-ordered workgroup waits only on
+// workgroups that are already running and publish before they wait, so every
+// wait ends; it is bounded all the same (late_ticks of the 100 MHz wall
+// clock, then kStatusLate: FMX_E_DEVICE, never a hang), and only launches
+// whose patterns are short enough that a tile's search is bounded take this
+// path (fmx_query.hip, launch_split).
 // The hand-off (MI355X_MICROARCH.md § visibility, the first row of the
 // sc1 table; cdna_hip_programming.md Guideline 16): one lane stores the
 // tile's count (an 8-B agent-scope relaxed store: sc1, write-through), waits
@@ -452,6 +456,9 @@ __device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
 __device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
     __hip_atomic_store((FMX_GLOBAL_AS uint64_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void st_agent32(uint32_t *p, uint32_t v) {
+    __hip_atomic_store((FMX_GLOBAL_AS uint32_t *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // every store of this wave has left it (inline asm: the compiler cannot drop it, Guideline 16 / the
 // compiler hazard of MI355X_MICROARCH.md § visibility)
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -460,6 +467,30 @@ __device__ __forceinline__ void poll_pause() { __builtin_amdgcn_s_sleep(2); }
 __device__ __forceinline__ void after_poll() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); }
 __device__ __forceinline__ uint64_t wall_ticks() { return wall_clock64(); }
 #endif
+
+// This workgroup's tile in batch jb: with grp.tickets (one 32-bit counter per
+// batch of the launch, zero before it: fmx_index::d_tickets, per status slot)
+// thread 0 takes the batch's next ticket; without, the tile is the
+// workgroup's index.  Read after the caller's next barrier (claim_tile).
+__device__ __forceinline__ void take_ticket(const LocateGroup &grp, uint32_t jb, uint32_t *s_tk) {
+    if (threadIdx.x == 0) *s_tk = grp.tickets ? atomicAdd(grp.tickets + jb, 1u) : blockIdx.x - grp.tile_begin[jb];
+}
+// After that barrier: the tile (workgroup-uniform), or G when the ticket is
+// out of range (a counter not zero at the launch: never expected; the
+// workgroup then answers nothing and the batch's waits end late, FMX_E_DEVICE,
+// and the host zeroes the slot's counters, read_status).  The workgroup that
+// took the batch's last ticket puts the counter back to zero: every other
+// ticket of the launch was taken before it.
+__device__ __forceinline__ uint32_t claim_tile(const LocateGroup &grp, uint32_t jb, uint64_t G, const uint32_t *s_tk,
+                                               uint32_t *status) {
+    const uint32_t g = __builtin_amdgcn_readfirstlane(*s_tk);
+    if (g >= G) {
+        if (threadIdx.x == 0) atomicOr(status, kStatusLate);
+        return (uint32_t)G;
+    }
+    if (grp.tickets && g + 1 == G && threadIdx.x == 0) st_agent32(grp.tickets + jb, 0u);
+    return g;
+}
 
 // Tile g's base offset in its batch (of G tiles) from the hand-off: publish
 // this tile's count agg (the last tile's is read by no one), then sum the
@@ -506,11 +537,15 @@ __global__ __launch_bounds__(256, VAR == kVarDerivedLong ? 4 : 8) void k_locate(
     __shared__ Tables<P> s;
     FMX_DYN_LDS(s_pat);  // stage_bytes, then the k-mer table (dynamic)
     __shared__ uint64_t s_scan[4], s_part[4];
-    stage_tables(a, s, s_pat + stage_bytes);
+    __shared__ uint32_t s_tk;
     const uint32_t jb = group_batch(grp, blockIdx.x);
+    take_ticket(grp, jb, &s_tk);
+    stage_tables(a, s, s_pat + stage_bytes);
+    __syncthreads();
     const LocateBatch &B = grp.b[jb];
     const uint64_t npat = B.npat, G = (npat + 255) / 256;
-    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
+    const uint32_t g = claim_tile(grp, jb, G, &s_tk, a.status);
+    if (g >= G) return;  // (workgroup-uniform)
     P lo, rloc;
     uint64_t mask;
     uint32_t mode;
@@ -1182,11 +1217,15 @@ __global__ __launch_bounds__(256) void k_emit_chain(const QueryArgs a, const Loc
                                                     uint64_t late_ticks) {
     __shared__ P sC[kMaxSigma + 1];
     __shared__ uint64_t s_scan[4], s_part[4];
-    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.tab->C[threadIdx.x];
+    __shared__ uint32_t s_tk;
     const uint32_t jb = group_batch(grp, blockIdx.x);
+    take_ticket(grp, jb, &s_tk);
+    if (threadIdx.x <= a.sigma) sC[threadIdx.x] = (P)a.tab->C[threadIdx.x];
+    __syncthreads();
     const LocateBatch &B = grp.b[jb];
     const uint64_t npat = B.npat, G = (npat + 255) / 256;
-    const uint32_t g = blockIdx.x - grp.tile_begin[jb];
+    const uint32_t g = claim_tile(grp, jb, G, &s_tk, a.status);
+    if (g >= G) return;  // (workgroup-uniform)
     const uint64_t i = (uint64_t)g * 256u + threadIdx.x;
     P lo = 0, rloc = 0;
     uint64_t mask = 0, cnt = 0;

@@ -75,6 +75,9 @@ __global__ __launch_bounds__(256) void k_scan(const LocateGroup grp) {
 __global__ __launch_bounds__(256) void k_group_scan(uint32_t *cnt) {
     __shared__ uint64_t s_scan[4];
     constexpr uint32_t per = 16;
+    // whole passes only: a partial last pass would read and write past the
+    // counters into the batch table that follows them
+    static_assert(kGroupCounterRoom % (256 * per) == 0, "kGroupCounterRoom must be a multiple of 4,096");
     uint32_t carry = 0;
     for (uint32_t base = 0; base < kGroupCounterRoom; base += 256 * per) {
         uint32_t v[per], sum = 0;
@@ -361,6 +364,14 @@ static uint64_t launch_tag() {
     return z ? z : 1;  // (0: what zeroed memory holds)
 }
 
+// The ticket counters of the launch's status slot (take_ticket), or null:
+// workgroup index order (FMX_FUSED_TICKETS=0, A/B).
+static uint32_t *slot_tickets(const fmx_index *ix, const QueryArgs &qa) {
+    if (!ix->fused_tickets || !ix->d_tickets || qa.status < ix->d_status || qa.status >= ix->d_status + kStatusSlots)
+        return nullptr;
+    return ix->d_tickets + (uint64_t)(qa.status - ix->d_status) * kMaxGroup;
+}
+
 // Bits per packed symbol for a grouped launch of the ng groups, or 0 when it
 // cannot be grouped (a batch without the fixed-length hint); *raw: some
 // batch's patterns do not pack into kGroupPackBits, so the sorted records
@@ -574,6 +585,7 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
     if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
     for (uint32_t g = 0; g < ng; ++g) {
         if (chain) {
+            grps[g].tickets = slot_tickets(ix, qa);
             e = d.ops->emit_chain(qa, d.vb, d.rec, grps[g], group_tiles(grps[g]), launch_tag(), ix->fused_late_ticks,
                                   stream);
         } else {
@@ -630,6 +642,7 @@ static hipError_t launch_split(const fmx_index *ix, const QueryArgs &qa, LocateG
     if (fused && stream_capturing(stream)) fused = false;
     hipError_t e;
     if (fused) {
+        grp.tickets = slot_tickets(ix, qa);
         if ((e = d.ops->locate(qa, d.vb, d.rec, search_var(qa, sb), grp, tiles, sb, launch_tag(),
                                ix->fused_late_ticks, stream)) != hipSuccess)
             return e;

@@ -118,6 +118,7 @@ class JobGather:
         # no collective (one rank): the slab is its own result
         self.out = [torch.zeros(self.world * s, dtype=dtype, device=device)
                     for s in self.slab] if self.collective else self.inp
+        self.outc = [None] * self.ngroups  # the `counts` gathers' slabs (made on first use)
 
     def _where(self, j: int):
         g = j // self.group
@@ -133,16 +134,46 @@ class JobGather:
         o = int(self.cnt[self.rank, g] + self.needs[self.rank, j0:j].sum())
         return self.inp[g][o:o + int(self.needs[self.rank, j])]
 
-    def gather(self, g: int, async_op: bool = False):
+    def counts_max(self, g: int) -> int:
+        """Group g's count part on the largest rank (the `counts` gather's slab)."""
+        return max(1, int(self.cnt[:, g].max()))
+
+    def gather(self, g: int, async_op: bool = False, part: str = "all"):
         """Group g's all-gather (enqueue it on a communication stream to
-        overlap it with the next launch); None with one rank."""
+        overlap it with the next launch); None with one rank.  part "all":
+        the whole slab (counts and locations); "counts": the counts alone
+        (every rank's first counts_max(g) words, into a slab of their own —
+        the job's offsets on every rank; the locations stay where they were
+        computed until a later "all" gather)."""
         if not self.collective:
             return None
+        if part == "counts":
+            import torch
+            c = self.counts_max(g)
+            if self.outc[g] is None:
+                self.outc[g] = torch.zeros(self.world * c, dtype=self.inp[g].dtype, device=self.inp[g].device)
+            return _all_gather_flat(self.outc[g], self.inp[g][:c], self.pg, async_op)
+        if part != "all":
+            raise ValueError(f"JobGather.gather: part {part!r} (all | counts)")
         return _all_gather_flat(self.out[g], self.inp[g], self.pg, async_op)
 
     def gather_all(self):
         for g in range(self.ngroups):
             self.gather(g)
+
+    def assemble_offsets(self):
+        """The job's offsets int64[total+1] from the `counts` gathers alone."""
+        import torch
+        cnts = []
+        for r in range(self.world):
+            for g in range(self.ngroups):
+                src = self.outc[g] if self.collective else self.inp[g]
+                b = r * self.counts_max(g) if self.collective else 0
+                cnts.append(src[b:b + int(self.cnt[r, g])])
+        counts = torch.cat(cnts).to(torch.int64)
+        offsets = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=counts.device)
+        torch.cumsum(counts, 0, out=offsets[1:])
+        return offsets
 
     def assemble(self):
         """The job's (offsets int64[total+1], locations) on the device, ranks
@@ -161,8 +192,11 @@ class JobGather:
         torch.cumsum(counts, 0, out=offsets[1:])
         return offsets, torch.cat(locs)
 
-    def bytes_per_pass(self) -> int:
-        """Bytes every rank receives per pass over the job (all groups)."""
+    def bytes_per_pass(self, part: str = "all") -> int:
+        """Bytes every rank receives per pass over the job (all groups), by
+        gather part ("all": whole slabs; "counts": the count slabs alone)."""
+        if part == "counts":
+            return sum(self.world * self.counts_max(g) for g in range(self.ngroups)) * self.elt
         return sum(self.world * s for s in self.slab) * self.elt
 
     def result_bytes(self) -> int:
@@ -272,17 +306,17 @@ class ShardedLocate:
 
 
 def workspace_bytes(n: int, pos_bytes: int) -> int:
-    """fmx_locate_workspace_size for n patterns (fmx_api.cpp ws_bytes_for):
-    [256 B + 4 x 8,192 key counters + a grouped launch's batch table (1,024
-    batches x 44 B)][tile counts and offsets: 2 x 8 B per 256-pattern
-    tile][search records: 16 B (u32) / 24 B (u64) per pattern][16 B][sorted
-    order: 16 B per pattern]."""
-    tiles = max(1, -(-int(n) // 256))
-    return (256 + 4 * 8192 + GROUP_TAB_BYTES + 16 * tiles + int(n) * (16 if pos_bytes == 4 else 24) + 16
-            + 16 * int(n))
-
-
-GROUP_TAB_BYTES = 1024 * (8 + 4 + 32)  # fmx_internal.hpp GroupTab (first, vfirst, desc per batch)
+    """fmx_locate_workspace_size for n patterns, from the library itself
+    (fmx_workspace_bytes, ABI 8: the same arithmetic as the index's, no
+    index needed) — so the per-rank accounting follows any build's key
+    counters, batch table (FMX_MAX_MEGA) and record sizes."""
+    import ctypes as C
+    from . import _native as _n
+    out = C.c_uint64()
+    st = _n.lib().fmx_workspace_bytes(int(n), int(pos_bytes), C.byref(out))
+    if st != 0:
+        raise ValueError(f"fmx_workspace_bytes({n}, {pos_bytes}): status {st}")
+    return int(out.value)
 
 
 def hbm_per_rank(*, blob: int, records: int, text: int, batch_sizes: Sequence[int], m: int, pos_bytes: int,

@@ -51,3 +51,30 @@ def occurrences(text_idx: bytes, pat_idx: bytes):
 
 def encode(table: bytes, data: bytes) -> bytes:
     return bytes(table[b] for b in data)
+
+
+# Full-size blob provenance (the C2-C5 blobs' SHA-256 recorded).
+# The text recipe is shared by tests/golden/make_blob_digests.py (the oracle's
+# CPU builder, in this container) and tests/test_gpu_provenance.py (the GPU
+# builder, on the box): numpy's PCG64 stream is the same on both.
+ACGTN_SYMBOLS = [b"Aa", b"Cc", b"Gg", b"Tt", b"Nn"]
+AMINO20 = b"ACDEFGHIKLMNPQRSTVWY"
+PROVENANCE = {
+    # name: (n, alphabet, symbols, (P bytes, planes, vector bits), seed)
+    "c2": (1_000_000_000, b"ACGT", ACGTN_SYMBOLS, (4, 3, 64), 20261),
+    "c4": (1_000_000_000, AMINO20, [bytes([c, c + 32]) for c in AMINO20] + [b"Xx"], (4, 5, 64), 20262),
+}
+PROVENANCE_K, PROVENANCE_SR = 3, 2
+
+
+def provenance_text(name):
+    """The seeded text of a provenance config: uniform over its alphabet."""
+    n, alphabet, _, _, seed = PROVENANCE[name]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.empty(n, dtype=np.uint8)
+    lut = np.frombuffer(alphabet, dtype=np.uint8)
+    step = 1 << 26
+    for c0 in range(0, n, step):
+        c1 = min(n, c0 + step)
+        out[c0:c1] = lut[rng.integers(0, len(alphabet), c1 - c0, dtype=np.uint8)]
+    return out

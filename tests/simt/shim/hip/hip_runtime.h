@@ -189,6 +189,10 @@ inline void st_agent(uint64_t *p, uint64_t v) {
     __atomic_store_n(p, v, __ATOMIC_RELAXED);
     ::simt::maybe_yield();
 }
+inline void st_agent32(uint32_t *p, uint32_t v) {
+    __atomic_store_n(p, v, __ATOMIC_RELAXED);
+    ::simt::maybe_yield();
+}
 inline void drain_stores() {}
 inline void poll_pause() { ::simt::maybe_yield(); }
 inline void after_poll() {}

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol(pkg):
     for name in declared:
         assert hasattr(lib, name), f"libfmx.so does not export {name}"
     assert set(declared) == set(pkg._native.SIGNATURES), "ctypes signatures out of sync with fmx.h"
-    assert lib.fmx_abi_version() == 7
+    assert lib.fmx_abi_version() == 8
 
 
 def test_status_strings(pkg):

@@ -74,7 +74,7 @@ def _worker(rank, world, port, result_path, group, batch_target):
     dist.destroy_process_group()
 
 
-def _weak_worker(rank, world, port, result_path, nb, B, group):
+def _weak_worker(rank, world, port, result_path, nb, B, group, policy="all"):
     """bench.py's c2 weak-scaling gather: every rank answers its own nb
     batches of B patterns (different patterns per rank), the outputs live in
     JobGather slots sized once from a sizing pass, and each launch group's
@@ -111,9 +111,12 @@ def _weak_worker(rank, world, port, result_path, nb, B, group):
         jg.counts_slot(j).copy_(torch.from_numpy(np.diff(o).astype(np.int32)))
         jg.locs_slot(j).copy_(torch.from_numpy(l.astype(np.int32)))
     for q in range(3 * jg.ngroups):  # launches cycle over the groups: one collective each
-        wk = jg.gather(q % jg.ngroups, async_op=q % 2 == 1)
+        wk = jg.gather(q % jg.ngroups, async_op=q % 2 == 1, part=policy)
         if wk is not None:
             wk.wait()
+    coff = jg.assemble_offsets() if policy == "counts" else None
+    if policy == "counts":
+        jg.gather_all()  # the locations once, after the passes (bench.py --gather counts)
     goff, glocs = jg.assemble()
     if rank == 0:
         allp = [text[s:s + m] for r in range(world) for s in starts[r]]
@@ -121,8 +124,11 @@ def _weak_worker(rank, world, port, result_path, nb, B, group):
         ref_off, ref_locs = ix.locate_batch(d, o)
         ok = (np.array_equal(goff.numpy().astype(np.uint64), ref_off)
               and np.array_equal(glocs.numpy().astype(np.uint32), ref_locs))
+        if coff is not None:
+            ok = ok and np.array_equal(coff.numpy().astype(np.uint64), ref_off)
         with open(result_path, "w") as f:
-            json.dump({"ok": bool(ok), "ratio": jg.bytes_per_pass() / jg.result_bytes(), "groups": jg.ngroups}, f)
+            json.dump({"ok": bool(ok), "ratio": jg.bytes_per_pass() / jg.result_bytes(), "groups": jg.ngroups,
+                       "counts_ratio": jg.bytes_per_pass("counts") / jg.bytes_per_pass()}, f)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -364,17 +370,43 @@ def test_gloo_job_gather_matches_single(tmp_path, world, group, target):
     assert r["ratio"] <= 1.25, r  # slabs padded only to the largest rank's share
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_weak_gather_in_step(tmp_path, world):
+@pytest.mark.parametrize("world,policy", [(2, "all"), (3, "all"), (2, "counts")])
+def test_gloo_weak_gather_in_step(tmp_path, world, policy):
     """c2 weak scaling's in-step gather (bench.py, VERDICT r3 missing #3):
     uniform batches per rank, one all-gather per launch, launches cycling over
-    the groups; exact result, padding <= 1.25x."""
+    the groups; exact result, padding <= 1.25x.  `counts` (bench.py --gather
+    counts): the in-step gathers move the count slabs
+    alone — the job's offsets, checked — and the locations are gathered once
+    afterwards; the assembled job is the same."""
     import torch.multiprocessing as mp
     out = tmp_path / "res.json"
-    mp.spawn(_weak_worker, args=(world, _free_port(), str(out), 6, 150, 2), nprocs=world, join=True)
+    mp.spawn(_weak_worker, args=(world, _free_port(), str(out), 6, 150, 2, policy), nprocs=world, join=True)
     r = json.loads(out.read_text())
     assert r["ok"] and r["groups"] == 3
     assert r["ratio"] <= 1.25, r
+    assert 0.3 < r["counts_ratio"] < 0.7, r  # (about one location per pattern: counts are about half)
+
+
+def test_weak_gather_volume_world8(pkg):
+    """The world-8 slab arithmetic of bench.py's c2 weak shape (VERDICT r5
+    next #4): 2 launch groups of 1,024 batches x 100,000 patterns per rank,
+    ~1 location per pattern; every rank receives 8 x its slab per launch
+    group.  `all`: 8 x 2 x ~0.83 GB = ~13 GB per pass and rank; `counts`:
+    half of it; the required xGMI rate per GPU at bench's ~25 ms per launch."""
+    import torch
+    D = pkg.distributed
+    world, GR, B = 8, 1024, 100_000
+    sizes = np.full((world, 2 * GR), B, dtype=np.int64)
+    needs = np.full((world, 2 * GR), B + 37, dtype=np.int64)  # ~1 location per 20-mer at 1 Gbp
+    jg = D.JobGather(sizes, needs, GR, 0, torch.int32, "cpu", collective=False)
+    slab = GR * (2 * B + 37) * 4
+    assert jg.slab == [GR * (2 * B + 37)] * 2
+    assert jg.bytes_per_pass() == world * 2 * slab
+    assert jg.bytes_per_pass("counts") == world * 2 * GR * B * 4
+    # the rate each policy needs per GPU if a launch group (102.4 M patterns) takes ~25 ms
+    need_all = jg.bytes_per_pass() / 2 / 25e-3 / 1e9
+    need_counts = jg.bytes_per_pass("counts") / 2 / 25e-3 / 1e9
+    assert 250 < need_all < 280 and 125 < need_counts < 140, (need_all, need_counts)
 
 
 def test_bench_refuses_oversubscribed_rccl():

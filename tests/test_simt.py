@@ -504,13 +504,14 @@ def test_grouping_policy_simt(pkg, O, simt, monkeypatch):
 @pytest.fixture
 def fused(simt, monkeypatch):
     """The fused launch (k_locate) and the chained grouped emit
-    (k_emit_chain) on, workgroups in index order — the order the GPU
-    dispatches them in, which their waits rely on."""
+    (k_emit_chain) on, workgroups run in a SHUFFLED order: a workgroup answers
+    the tile of its ticket (take_ticket, the number of its batch's workgroups
+    started before it), so it only ever waits on tiles already running and
+    the launch needs no dispatch order at all."""
     monkeypatch.setenv("FMX_FUSED", "1")
     monkeypatch.setenv("FMX_EMIT_CHAIN", "1")
-    simt.simt_block_order(1)
-    yield simt
     simt.simt_block_order(0)
+    yield simt
 
 
 def fused_case(O, rng, pb, planes, vb, sigma, n_text):
@@ -606,13 +607,17 @@ def test_fused_group_garbage_workspaces_simt(pkg, O, fused, monkeypatch):
 
 
 def test_fused_wait_is_bounded_simt(pkg, O, simt, monkeypatch):
-    """k_locate's waits end: with workgroups run in a shuffled order (a later
-    tile before an earlier one, which the GPU's in-order dispatch never does)
-    the waiting workgroups give up after FMX_FUSED_TIMEOUT_MS and the launch
-    reports FMX_E_DEVICE instead of hanging; the next launch, dispatched in
-    order, answers correctly."""
+    """k_locate's waits end.  Without tickets (FMX_FUSED_TICKETS=0: each
+    workgroup answers the tile of its index) and workgroups run in a shuffled
+    order (a later tile before an earlier one, one workgroup at a time: the
+    residency trap of ADVICE r5 in its extreme form) the waiting workgroups
+    give up after FMX_FUSED_TIMEOUT_MS and the launch reports FMX_E_DEVICE
+    instead of hanging; the next launch, dispatched in order, answers
+    correctly.  With tickets (the default) the same shuffled launch answers
+    correctly: every tile waits only on tiles whose workgroups already ran."""
     monkeypatch.setenv("FMX_FUSED", "1")
     monkeypatch.setenv("FMX_FUSED_TIMEOUT_MS", "20")
+    monkeypatch.setenv("FMX_FUSED_TICKETS", "0")
     simt.simt_config(99, 0.5)
     rng = np.random.default_rng(3)
     chars, text, blob = fused_case(O, rng, 4, 3, 64, 4, 3000)
@@ -620,6 +625,7 @@ def test_fused_wait_is_bounded_simt(pkg, O, simt, monkeypatch):
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
     pats = [text[s:s + 9] for s in rng.integers(0, len(text) - 9, size=8 * 256)]
     data, offsets = pkg.pack_patterns(pats)
+    ooff, olocs = orc.locate_batch(data, offsets)
     with pytest.raises(pkg.FmxError) as ei:
         ix.locate_batch((data, offsets))
     assert ei.value.code == pkg._native.FMX_E_DEVICE
@@ -628,8 +634,15 @@ def test_fused_wait_is_bounded_simt(pkg, O, simt, monkeypatch):
         goff, glocs = ix.locate_batch((data, offsets))
     finally:
         simt.simt_block_order(0)
-    ooff, olocs = orc.locate_batch(data, offsets)
     assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs)
+    ix.close()
+    monkeypatch.setenv("FMX_FUSED_TICKETS", "1")
+    ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
+    for rep in range(3):  # (shuffled; the counters back at zero after every launch)
+        goff, glocs = ix.locate_batch((data, offsets))
+        assert np.array_equal(goff, ooff) and np.array_equal(glocs, olocs), f"tickets, launch {rep}"
+    # (the host API may launch a batch twice: its first output guess too small)
+    assert ix.info()["launches_fused"] == ix.info()["launches_ordered"] >= 3
     ix.close()
 
 
