@@ -47,6 +47,9 @@
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   megatest test_gpu_mega.py (1,024-batch grouped launch, two-stream fused launches), test_gpu_fused.py,
 #            test_gpu_provenance.py
+#   c4pair   C4 one vs two patterns per lane in the grouped search, alternating twice; C2 two per lane once
+#   shapes   the per-rank shapes of C3 (10 M / N) and C5 (1 M / N) at N = 1, 2, 4, 8 on one GPU
+#   gloo2g   bench.py --gpus 2 over gloo on the one GPU with --gather all and --gather counts
 #   ticketab the fused launch's tickets vs workgroup index order: single batch and C1, alternating twice
 #   fusedab  the fused launch vs the two-kernel path (FMX_FUSED=0): single batch, C1, C4, alternating twice;
 #            then the single-batch kernel trace of the fused build
@@ -323,6 +326,29 @@ for step in "$@"; do
                 run "c1_tk_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
                 FMX_FUSED_TICKETS=0 run "c1_idx_$r" 300 python -u bench.py --config c1 --no-cpu || exit 1
             done ;;
+        c4pair)  # C4 (grouped, 1,024 per launch): one vs two patterns per lane in the grouped search
+            # (FMX_GROUPED_PAIR=1), alternating twice; then C2 with two per lane once
+            B="python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "c4_k1_$r" 400 $B || exit 1
+                FMX_GROUPED_PAIR=1 run "c4_k2_$r" 400 $B || exit 1
+            done
+            FMX_GROUPED_PAIR=1 run c2_k2 400 python -u bench.py --no-cpu --no-blob-layout --no-single-batch || exit 1
+            run c2_k1 400 python -u bench.py --no-cpu --no-blob-layout --no-single-batch || exit 1 ;;
+        shapes)  # the per-rank shapes JobPlan deals at N = 1/2/4/8, each run on this one GPU (no gathers):
+            # C3 10 M / N and C5 1 M / N patterns; and C3's N = 8 slab in launch order
+            B="--no-cpu --no-blob-layout --no-single-batch"
+            for t in 10000000 5000000 2500000 1250000; do
+                run "c3_t$t" 400 python -u bench.py --config c3 --total-patterns $t $B || exit 1
+            done
+            FMX_GROUPED=0 run c3_t1250000_lo 400 python -u bench.py --config c3 --total-patterns 1250000 $B || exit 1
+            for t in 1000000 500000 250000 125000; do
+                run "c5_t$t" 500 python -u bench.py --config c5 --total-patterns $t $B || exit 1
+            done ;;
+        gloo2g)  # two gloo ranks on the one GPU, c2 weak, both gather policies
+            FMX_BENCH_BACKEND=gloo run bench_gloo2_all 600 python -u bench.py --gpus 2 --no-cpu --gather all || exit 1
+            FMX_BENCH_BACKEND=gloo run bench_gloo2_counts 600 python -u bench.py --gpus 2 --no-cpu --gather counts \
+                || exit 1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
