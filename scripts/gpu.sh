@@ -47,6 +47,7 @@
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   megatest test_gpu_mega.py (1,024-batch grouped launch, two-stream fused launches), test_gpu_fused.py,
 #            test_gpu_provenance.py
+#   c4walk   C4 with vs without the walk line in its multi-line records, alternating twice
 #   c4pair   C4 one vs two patterns per lane in the grouped search, alternating twice; C2 two per lane once
 #   shapes   the per-rank shapes of C3 (10 M / N) and C5 (1 M / N) at N = 1, 2, 4, 8 on one GPU
 #   gloo2g   bench.py --gpus 2 over gloo on the one GPU with --gather all and --gather counts
@@ -349,6 +350,14 @@ for step in "$@"; do
             FMX_BENCH_BACKEND=gloo run bench_gloo2_all 600 python -u bench.py --gpus 2 --no-cpu --gather all || exit 1
             FMX_BENCH_BACKEND=gloo run bench_gloo2_counts 600 python -u bench.py --gpus 2 --no-cpu --gather counts \
                 || exit 1 ;;
+        c4walk)  # C4 (grouped, 1,024 per launch): multi-line symbol masks with a walk line (FMX_OCC_WALK=1,
+            # 4 x 128 B per 64 rows) vs without (3 x 128 B: the walk reads the planes, then the symbol's unit),
+            # alternating twice; then one-stream kernel traces of each
+            B="python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                FMX_OCC_WALK=0 run "c4_nowalk_$r" 400 $B || exit 1
+                FMX_OCC_WALK=1 run "c4_walk_$r" 400 $B || exit 1
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

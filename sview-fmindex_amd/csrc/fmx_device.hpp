@@ -154,14 +154,29 @@ using V4 = uint32_t __attribute__((ext_vector_type(4)));
 //            sit verbatim at the record's end (last line's spare bytes) for
 //            the walk, which needs the symbol before it can pick a unit
 //            (C4: sigma 21, three lines, 384 B per 64 rows).
+// REC = (256..512)|kRecOneHot|kRecWalk — multi-line symbol masks with a WALK
+//            LINE (round 6): the units fill lines 0 .. L-2 (PL per line, as
+//            above), and the last line is the block's plain record — planes
+//            verbatim at [0, PB), the block's own sigma checkpoints at PBA +
+//            c*P — so that the walk's get_pre_rank_and_symidx reads one line
+//            (the symbol from the planes, its checkpoint beside them) instead
+//            of the planes and then the symbol's unit: one dependent round
+//            trip per walk step instead of two.  Where PBA + sigma*P <= 128
+//            (C4: 40 + 84 B; four lines, 512 B per 64 rows).
 constexpr int kRecPaired = 1;
 constexpr int kRecOneHot = 2;
+constexpr int kRecWalk = 4;
 
 // Whether record encoding rec (0, 64, 128, | kRecPaired, | kRecOneHot) can
 // hold a block of N planes of VB bits and at least one checkpoint of pos bytes.
 constexpr bool rec_fits(int pos, int N, int VB, int rec) {
     const int pb = N * VB / 8, rb = rec & ~15;
     if (rec == 0) return true;
+    if (rec & kRecWalk) {  // units in lines 0 .. L-2, the block's plain record in the last line
+        const int u = VB / 8 + pos, pba = (pb + pos - 1) / pos * pos;
+        return (rec & kRecOneHot) && u % 4 == 0 && rb % 128 == 0 && rb >= 256 && rb <= 512 && u <= 128 &&
+               pba + pos <= 128 && (1 << N) * u > 128;
+    }
     if (rec & kRecOneHot) {
         const int u = VB / 8 + pos;
         if (u % 4 != 0) return false;
@@ -188,8 +203,12 @@ struct Occ {
     static constexpr int PER = PAIRED ? (16 - PTA) / (int)sizeof(P) : 1;       // checkpoints per paired chunk
     static constexpr int NCH = RB / 16;                                        // chunks per record
     static constexpr bool MULTI = ONEHOT && RB > 128;                        // multi-line symbol masks
+    static constexpr bool WALK = MULTI && (REC & kRecWalk) != 0;              // ... with a walk line
     static constexpr int PL = RB > 128 ? 128 / U : RB / (U > 0 ? U : 1);       // units per line
+    static constexpr int NCKW = (128 - PBA) / (int)sizeof(P);                  // walk line: checkpoint slots
+    static constexpr int NCKW2 = pow2_ceil(NCKW);
     static constexpr int NCK = REC == 0 ? (1 << N)
+                             : WALK     ? (RB / 128 - 1) * PL
                              : MULTI    ? (RB / 128 - 1) * PL + (128 - PB) / U
                              : ONEHOT   ? RB / U
                              : PAIRED   ? (NCH - PF) * PER
@@ -403,6 +422,24 @@ struct Occ {
                 c = pl.sym(rem);
                 return ckq[c] + (P)pl.rank(rem, c);
             }
+        } else if constexpr (WALK) {
+            // the walk line (the block's plain record): planes and every
+            // checkpoint in one round trip, the symbol's picked in registers
+            const V4 *rp = reinterpret_cast<const V4 *>(a.occ + q * RB + (RB - 128));
+            V4 ch[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ch[i] = rp[i];
+            planes_from(ch, pl);
+            c = pl.sym(rem);
+            P all[NCKW2];
+#pragma unroll
+            for (int i = 0; i < NCKW2; ++i) {
+                const int d = (PBA + i * (int)sizeof(P)) / 4;
+                if (i >= NCKW) all[i] = P(0);
+                else if constexpr (sizeof(P) == 8) all[i] = (P)((uint64_t)dw(ch, d) | (uint64_t)dw(ch, d + 1) << 32);
+                else all[i] = (P)dw(ch, d);
+            }
+            return tree_pick<NCKW2>(all, c) + (P)pl.rank(rem, c);
         } else if constexpr (MULTI) {
             // the symbol from the planes kept at the record's end, then its unit
             pl.load(a.occ + q * RB + (RB - PB));
@@ -447,7 +484,7 @@ struct Occ {
 // faithful index, the derived kernels are not built for them): paired-chunk records when the planes leave a tail and they fit the
 // record size the plain layout would take (never larger), else plain 64/128.
 FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits, uint32_t sigma,
-                                      bool paired = true, bool onehot = true, bool multi = true) {
+                                      bool paired = true, bool onehot = true, bool multi = true, bool walk = false) {
     const uint32_t pb = planes * vec_bits / 8;
     const uint32_t pba = (pb + pos_bytes - 1) / pos_bytes * pos_bytes;
     const uint32_t need = pba + sigma * pos_bytes;
@@ -455,6 +492,12 @@ FMX_HD uint32_t interleaved_rec_bytes(uint32_t pos_bytes, uint32_t planes, uint3
     const uint32_t u = vec_bits / 8 + pos_bytes, hb = sigma * u;
     const uint32_t hot = hb <= 64 ? 64u : hb <= 128 ? 128u : 0u;
     if (onehot && hot != 0 && u % 4 == 0 && (plain == 0 || hot <= plain)) return hot | (uint32_t)kRecOneHot;
+    if (onehot && multi && walk && hot == 0 && u % 4 == 0 && pba + sigma * pos_bytes <= 128) {
+        // units in lines 0 .. l-2, the block's plain record (planes + sigma checkpoints) as the last line
+        const uint32_t pl = 128 / u;
+        for (uint32_t l = 2; l <= 4; ++l)
+            if (sigma <= (l - 1) * pl) return 128 * l | (uint32_t)kRecOneHot | (uint32_t)kRecWalk;
+    }
     if (onehot && multi && hot == 0 && u % 4 == 0 && u <= 128 - pb) {
         // multi-line: PL units per line, the planes in the last line's spare bytes
         const uint32_t pl = 128 / u, last_cap = (128 - pb) / u;
@@ -487,8 +530,15 @@ FMX_HD void write_record(uint8_t *dst, const uint8_t *planes, const uint8_t *ckr
         // unit c: the AND over planes j of plane j (bit j of c set) or its
         // complement — Block::get_remain_count_of's mask — then checkpoint c
         constexpr int MW = VB / 32;  // mask dwords
-        if constexpr (O::MULTI)
+        if constexpr (O::WALK) {
+            // the walk line: planes, then this block's checkpoints (rank_checkpoints[q*sigma + c])
+            constexpr int WL = (RB - 128) / 4;
+            for (int i = 0; i < O::PB / 4; ++i) w[WL + i] = pw[i];
+            for (uint32_t i = 0; i < sigma * (uint32_t)CW && i < (uint32_t)(128 - O::PBA) / 4; ++i)
+                w[WL + O::PBA / 4 + i] = cw[i];
+        } else if constexpr (O::MULTI) {
             for (int i = 0; i < O::PB / 4; ++i) w[(RB - O::PB) / 4 + i] = pw[i];
+        }
         for (int c = 0; c < O::NCK; ++c) {  // (load time only; not unrolled)
             if ((uint32_t)c >= sigma) break;
             const int ub = O::MULTI ? (c / O::PL) * 32 + (c % O::PL) * (O::U / 4) : c * (O::U / 4);  // unit dword

@@ -109,6 +109,12 @@ struct QueryArgs {
 };
 
 constexpr uint8_t kNoDigit = 0xFF;
+// Multi-line symbol-mask records with a walk line (fmx_device.hpp kRecWalk)
+// by default (FMX_OCC_WALK=0 / 1 at load overrides; build option for A/B)
+#ifndef FMX_OCC_WALK_DEFAULT
+#define FMX_OCC_WALK_DEFAULT 0
+#endif
+constexpr bool kOccWalkDefault = FMX_OCC_WALK_DEFAULT != 0;
 constexpr uint32_t kStatusSlots = 1024;   // status words per index (one per stream)
 constexpr uint64_t kKmerLdsMax = 4096;    // k-mer count tables up to this size are staged in LDS
 

@@ -36,6 +36,9 @@ hipError_t disp_rec(uint32_t rec, F &&f) {
         case 256 | kRecOneHot: return disp_if<VB, 256 | kRecOneHot>(f);
         case 384 | kRecOneHot: return disp_if<VB, 384 | kRecOneHot>(f);
         case 512 | kRecOneHot: return disp_if<VB, 512 | kRecOneHot>(f);
+        case 256 | kRecOneHot | kRecWalk: return disp_if<VB, 256 | kRecOneHot | kRecWalk>(f);
+        case 384 | kRecOneHot | kRecWalk: return disp_if<VB, 384 | kRecOneHot | kRecWalk>(f);
+        case 512 | kRecOneHot | kRecWalk: return disp_if<VB, 512 | kRecOneHot | kRecWalk>(f);
         default: return hipErrorInvalidValue;
     }
 }

@@ -231,6 +231,12 @@ int by_rec(uint32_t rec, const orc_index &ox, uint32_t options, const uint8_t *b
         case 256 | kRecOneHot: return run_if<P, N, VB, 256 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
         case 384 | kRecOneHot: return run_if<P, N, VB, 384 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
         case 512 | kRecOneHot: return run_if<P, N, VB, 512 | kRecOneHot>(ox, options, b, o, n, f, c, l, cap, need);
+        case 256 | kRecOneHot | kRecWalk:
+            return run_if<P, N, VB, 256 | kRecOneHot | kRecWalk>(ox, options, b, o, n, f, c, l, cap, need);
+        case 384 | kRecOneHot | kRecWalk:
+            return run_if<P, N, VB, 384 | kRecOneHot | kRecWalk>(ox, options, b, o, n, f, c, l, cap, need);
+        case 512 | kRecOneHot | kRecWalk:
+            return run_if<P, N, VB, 512 | kRecOneHot | kRecWalk>(ox, options, b, o, n, f, c, l, cap, need);
         default: return run<P, N, VB, 0>(ox, options, b, o, n, f, c, l, cap, need);
     }
 }
@@ -267,7 +273,8 @@ extern "C" {
 
 // options: the fmx_load bit field (1 interleaved, 2 deep LUT, 4 full SA, 8 text,
 // 16 row contexts, 32 single-row deep-table entries; 64 here: plain records,
-// neither paired-chunk nor symbol-mask); bits 8.. = the scan limit
+// neither paired-chunk nor symbol-mask; bit 30 here: multi-line symbol masks
+// with a walk line where they fit); bits 8.. = the scan limit
 // (FMX_SCAN_ROWS, 0 = default 32).
 // Outputs are u64: counts[npat] and the concatenated locations.
 int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t planes, uint32_t vec_bits,
@@ -279,9 +286,9 @@ int emu_locate(const uint8_t *blob, uint64_t len, uint32_t pos_bytes, uint32_t p
     if (st) return st;
     // the loader's record choice (fmx_load / k_relayout): option bit 64 keeps
     // plain records; multi-line symbol masks only without derived structures
-    const bool fancy = (options & 64u) == 0, multi = fancy && (options & 62u) == 0;
+    const bool fancy = (options & 64u) == 0, multi = fancy && (options & 62u) == 0, walk = (options & (1u << 30)) != 0;
     const uint32_t rec =
-        (options & 1u) ? interleaved_rec_bytes(pos_bytes, planes, vec_bits, ox.sigma, fancy, fancy, multi) : 0u;
+        (options & 1u) ? interleaved_rec_bytes(pos_bytes, planes, vec_bits, ox.sigma, fancy, fancy, multi, walk) : 0u;
     using Run = int (*)(EMU_ARGS);
     static const Run tab[2][5] = {{emu_run_4_2, emu_run_4_3, emu_run_4_4, emu_run_4_5, emu_run_4_6},
                                   {emu_run_8_2, emu_run_8_3, emu_run_8_4, emu_run_8_5, emu_run_8_6}};

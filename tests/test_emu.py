@@ -17,10 +17,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 EMU = os.path.join(HERE, "emu", "libfmx_emu.so")
 # fmx_load option bits; bits 8.. set the row-scan limit (FMX_SCAN_ROWS)
 # (bit 7: the long-pattern kernels' vectorised tail compare instead of the short one;
-#  bit 6: plain interleaved records where the loader would pick paired-chunk or symbol-mask ones)
+#  bit 6: plain interleaved records where the loader would pick paired-chunk or symbol-mask ones;
+#  bit 30: multi-line symbol masks with a walk line where they fit, fmx_device.hpp kRecWalk)
 OPTIONS = (0, 1, 1 | 64, 31 | 64, 1 | 2, 1 | 4, 1 | 2 | 4 | 8, 4 | 8, 2 | 8, 31, 16, 1 | 16 | (1 << 8), 2 | 16 | (64 << 8),
            1 | 2 | 16 | (5 << 8), 2 | 8 | 32, 63, 1 | 2 | 16 | 32 | (3 << 8),
-           4 | 8 | 128, 31 | 128, 63 | 128, 1 | 2 | 16 | 32 | 128 | (3 << 8))
+           4 | 8 | 128, 31 | 128, 63 | 128, 1 | 2 | 16 | 32 | 128 | (3 << 8),
+           1 | (1 << 30))
 
 
 @pytest.fixture(scope="module")

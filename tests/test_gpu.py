@@ -215,15 +215,20 @@ def test_builder_and_queries_every_layout(pkg, O, pb, planes, vb):
             check_parity(pkg, O, blob, pb, planes, vb, 0, pats, occ)
 
 
-def expected_occ_record(pb, planes, vb, sigma, paired=True, onehot=True):
+def expected_occ_record(pb, planes, vb, sigma, paired=True, onehot=True, walk=False):
     """The loader's record encoding (fmx_device.hpp interleaved_rec_bytes)."""
     b = planes * vb // 8
-    need = -(-b // pb) * pb + sigma * pb
+    pba = -(-b // pb) * pb
+    need = pba + sigma * pb
     plain = 64 if need <= 64 else 128 if need <= 128 else 0
     u = vb // 8 + pb
     hot = 64 if sigma * u <= 64 else 128 if sigma * u <= 128 else 0
     if onehot and hot and u % 4 == 0 and (plain == 0 or hot <= plain):
         return hot | 2
+    if onehot and walk and not hot and u % 4 == 0 and pba + sigma * pb <= 128:   # + a walk line
+        for lines in (2, 3, 4):
+            if sigma <= (lines - 1) * (128 // u):
+                return 128 * lines | 2 | 4
     if onehot and not hot and u % 4 == 0 and u <= 128 - b:   # multi-line symbol masks
         for lines in (2, 3, 4):
             if sigma <= (lines - 1) * (128 // u) + (128 - b) // u:
@@ -240,7 +245,8 @@ def expected_occ_record(pb, planes, vb, sigma, paired=True, onehot=True):
 @pytest.mark.parametrize("pb,planes,vb", ALL_LAYOUTS)
 def test_record_encodings(pkg, O, pb, planes, vb, monkeypatch):
     """Interleaved occ records — symbol-mask (one unit per symbol: its mask
-    over the block + checkpoint), paired-chunk (every rank reads planes + one
+    over the block + checkpoint; multi-line ones with or without a walk line,
+    FMX_OCC_WALK), paired-chunk (every rank reads planes + one
     checkpoint chunk that repeats the planes' tail) and plain
     (FMX_OCC_ONEHOT=0, FMX_OCC_PAIRED=0): the loader picks the expected
     encoding and each answers like the oracle, on random texts and on texts
@@ -253,12 +259,14 @@ def test_record_encodings(pkg, O, pb, planes, vb, monkeypatch):
                      chars + chars[:1] * 700 + chars * 3 + chars[-1:] * 300 + chars[1:2] * 257):
             blob = gpu_build(pkg, text, sigma, pb, planes, vb, 3 if sigma < 8 else 2, 2, table)
             pats = [rand_pattern(rng, text, 1, 24) for _ in range(300)] + [chars[:1] * 3, chars[-1:] * 5]
-            for onehot, paired in ((True, True), (False, True), (False, False)):
+            for onehot, paired, walk in ((True, True, False), (True, True, True), (False, True, False),
+                                         (False, False, False)):
                 monkeypatch.setenv("FMX_OCC_ONEHOT", "1" if onehot else "0")
                 monkeypatch.setenv("FMX_OCC_PAIRED", "1" if paired else "0")
+                monkeypatch.setenv("FMX_OCC_WALK", "1" if walk else "0")
                 ix = pkg.FmIndex.load(blob, pos_of(pkg, pb), block_of(pkg, planes, vb), options=1)
-                want = expected_occ_record(pb, planes, vb, sigma, paired, onehot)
-                assert ix.info()["occ_record"] == want, (sigma, onehot, paired)
+                want = expected_occ_record(pb, planes, vb, sigma, paired, onehot, walk)
+                assert ix.info()["occ_record"] == want, (sigma, onehot, paired, walk)
                 ix.close()
                 check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1)
                 check_parity(pkg, O, blob, pb, planes, vb, 0, pats, 1 | 2 | 4)
