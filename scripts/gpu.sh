@@ -47,6 +47,12 @@
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   megatest test_gpu_mega.py (1,024-batch grouped launch, two-stream fused launches), test_gpu_fused.py,
 #            test_gpu_provenance.py
+#   thresh   C3 slabs of 5 M / 2.5 M / 1.6 M / 1.25 M patterns: grouped vs launch order
+#   tabab    C2 on this build vs lib/ab/libfmx_prev.so (the previous commit), alternating twice
+#   c4       bench.py --config c4 (with the CPU leg)
+#   records  the record-encoding, every-layout, golden and README GPU tests
+#   m2048ab  C2 at 2,048 batches per launch (the FMX_MAX_MEGA=2048 build) vs 1,024, alternating twice
+#   tcc      the TCC hit/miss PMC pass alone (C2, shipped launch shape)
 #   c4walk   C4 with vs without the walk line in its multi-line records, alternating twice
 #   c4pair   C4 one vs two patterns per lane in the grouped search, alternating twice; C2 two per lane once
 #   shapes   the per-rank shapes of C3 (10 M / N) and C5 (1 M / N) at N = 1, 2, 4, 8 on one GPU
@@ -358,6 +364,34 @@ for step in "$@"; do
                 FMX_OCC_WALK=0 run "c4_nowalk_$r" 400 $B || exit 1
                 FMX_OCC_WALK=1 run "c4_walk_$r" 400 $B || exit 1
             done ;;
+        m2048ab)  # C2: 2,048 batches per grouped launch (sview-fmindex_amd/lib/ab/libfmx_m2048.so, -DFMX_MAX_MEGA=2048)
+            # vs the shipped 1,024, alternating twice (same box)
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "g1024_$r" 400 $B || exit 1
+                FMX_LIB=$PWD/sview-fmindex_amd/lib/ab/libfmx_m2048.so run "g2048_$r" 400 $B --group 2048 || exit 1
+            done ;;
+        tcc)  # the L2 hit / miss pass alone on C2 at the shipped launch shape (PMC_CONFIG for another config)
+            P="--config ${PMC_CONFIG:-c2} --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+            run pmc_tcc 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$OUT/pmc_tcc" -o run \
+                --output-format csv -- python3 -u bench.py $P || exit 1
+            shrink "$OUT/pmc_tcc" ;;
+        thresh)  # where grouping starts to pay for C3's per-rank slabs: grouped (FMX_GROUPED=1) vs launch order
+            # (FMX_GROUPED=0) at 5 M / 2.5 M / 1.6 M / 1.25 M patterns per launch (256 batches)
+            B="--no-cpu --no-blob-layout --no-single-batch"
+            for t in 5000000 2500000 1600000 1250000; do
+                FMX_GROUPED=1 run "c3g_t$t" 400 python -u bench.py --config c3 --total-patterns $t $B || exit 1
+                FMX_GROUPED=0 run "c3o_t$t" 400 python -u bench.py --config c3 --total-patterns $t $B || exit 1
+            done ;;
+        tabab)  # C2: this build (compact GroupTab copies) vs sview-fmindex_amd/lib/ab/libfmx_prev.so, alternating twice
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "tab_new_$r" 400 $B || exit 1
+                FMX_LIB=$PWD/sview-fmindex_amd/lib/ab/libfmx_prev.so run "tab_prev_$r" 400 $B || exit 1
+            done ;;
+        c4)  run bench_c4 400 python -u bench.py --config c4 || exit 1 ;;
+        records) run pytest_records 600 python -u -m pytest tests/test_gpu.py -k "record or every_layout or golden or readme" \
+                -x -v --timeout 300 --timeout-method thread || exit 1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

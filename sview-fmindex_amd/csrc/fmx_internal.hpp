@@ -110,9 +110,11 @@ struct QueryArgs {
 
 constexpr uint8_t kNoDigit = 0xFF;
 // Multi-line symbol-mask records with a walk line (fmx_device.hpp kRecWalk)
-// by default (FMX_OCC_WALK=0 / 1 at load overrides; build option for A/B)
+// by default: C4 3.858 / 3.866 vs 3.661 / 3.657 x 10^9 without (same box,
+// alternating, profiles/r6/r6b_c4_{walk,nowalk}_*); FMX_OCC_WALK=0 / 1 at
+// load overrides; build option for A/B
 #ifndef FMX_OCC_WALK_DEFAULT
-#define FMX_OCC_WALK_DEFAULT 0
+#define FMX_OCC_WALK_DEFAULT 1
 #endif
 constexpr bool kOccWalkDefault = FMX_OCC_WALK_DEFAULT != 0;
 constexpr uint32_t kStatusSlots = 1024;   // status words per index (one per stream)
@@ -463,7 +465,14 @@ struct GroupDesc {
 };
 struct GroupTab {
     uint64_t first[kMaxMega];   // the launch's sorted positions (= patterns) before batch j
-    uint32_t vfirst[kMaxMega];  // batch j's first pattern id
+    // the compact copies the search's workgroups stage into LDS (one contiguous
+    // upload): vfirst[j] = batch j's first pattern id, first32 = first (a
+    // launch's positions fit 32 bits: is_grouped), stride16 = its pattern
+    // length — 80 lines per workgroup prologue at 1,024 batches, where
+    // first (u64) and desc[].stride (one line per 4 entries) took 352 (round 6)
+    uint32_t vfirst[kMaxMega];
+    uint32_t first32[kMaxMega];
+    uint16_t stride16[kMaxMega];
     GroupDesc desc[kMaxMega];
 };
 constexpr uint64_t kWsGroupTab = 256 + 4ull * kGroupCounterRoom;  // (16-B aligned)

@@ -969,10 +969,10 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
         s_dig[threadIdx.x] =
             threadIdx.x < a.sigma && a.tab->dig[threadIdx.x] != kNoDigit ? a.tab->dig[threadIdx.x] : 0;
     const GroupTab &gt = *grp.gtab;
-    for (uint32_t j = threadIdx.x; j < grp.gn; j += 256) {
-        s_first[j] = (uint32_t)gt.first[j];
+    for (uint32_t j = threadIdx.x; j < grp.gn; j += 256) {  // (the compact copies: 10 B per batch)
+        s_first[j] = gt.first32[j];
         s_vfirst[j] = gt.vfirst[j];
-        s_stride[j] = (uint16_t)gt.desc[j].stride;
+        s_stride[j] = gt.stride16[j];
     }
     __syncthreads();
     // xcd: workgroup b takes chunk start(b % 8) + b / 8, so that (under the

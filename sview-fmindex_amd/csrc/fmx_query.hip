@@ -24,6 +24,7 @@
 // lo and hi share a block.
 #include <atomic>
 #include <chrono>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <random>
@@ -481,6 +482,8 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
             B.first = first;
             tab->first[gn] = first;
             tab->vfirst[gn] = (vt + grp.tile_begin[j]) * 256u;
+            tab->first32[gn] = (uint32_t)first;
+            tab->stride16[gn] = (uint16_t)B.stride;
             tab->desc[gn] = GroupDesc{reinterpret_cast<uint8_t *>(B.tiles + 2 * G),
                                       reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + ((B.npat * rb + 15) & ~15ull),
                                       B.bytes, B.stride, B.rev};
@@ -509,8 +512,13 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
     // before the count pass on the stream
     hipError_t e = hipMemsetAsync(gcount, 0, 4ull * kGroupCounterRoom, stream);
     if (e != hipSuccess) return e;
+    // (vfirst, first32 and stride16 are contiguous: one upload of the three)
+    static_assert(offsetof(GroupTab, first32) == offsetof(GroupTab, vfirst) + 4 * kMaxMega &&
+                      offsetof(GroupTab, stride16) == offsetof(GroupTab, first32) + 4 * kMaxMega,
+                  "GroupTab: vfirst, first32, stride16 contiguous");
     if ((e = put_bytes(d_tab->first, tab->first, 8ull * gn, stream)) != hipSuccess ||
-        (e = put_bytes(d_tab->vfirst, tab->vfirst, 4ull * gn, stream)) != hipSuccess ||
+        (e = put_bytes(d_tab->vfirst, tab->vfirst, offsetof(GroupTab, stride16) - offsetof(GroupTab, vfirst) +
+                       2ull * gn, stream)) != hipSuccess ||
         (e = put_bytes(d_tab->desc, tab->desc, sizeof(GroupDesc) * gn, stream)) != hipSuccess)
         return e;
     // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the

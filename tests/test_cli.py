@@ -226,7 +226,7 @@ def test_c_host_links_and_reports_abi(pkg):
         import __graft_entry__ as g
         g.build_c_host()
     p = subprocess.run([C_HOST, "--abi"], capture_output=True, text=True, timeout=60)
-    assert p.returncode == 0 and p.stdout.strip() == "fmx ABI 7"
+    assert p.returncode == 0 and p.stdout.strip() == "fmx ABI 8"
 
 
 @pytest.mark.gpu
