@@ -247,7 +247,7 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
  * last symbols, so that patterns whose backward searches share their first
  * LF steps run side by side, and searches them in that order — same
  * results.  Grouped by default: launches (a group call's batches together) of
- * at least 2^20 fixed-length patterns that pack into 96 bits, on the
+ * at least 3 x 2^20 fixed-length patterns that pack into 96 bits, on the
  * faithful index, when the key spans at least 5 symbols (DNA: 6), of at
  * least 2^26 when it spans fewer (20 residues: 3; environment
  * at load: FMX_GROUPED=0 never, =1 always — longer patterns too, with

@@ -390,6 +390,8 @@ for step in "$@"; do
                 FMX_LIB=$PWD/sview-fmindex_amd/lib/ab/libfmx_prev.so run "tab_prev_$r" 400 $B || exit 1
             done ;;
         c4)  run bench_c4 400 python -u bench.py --config c4 || exit 1 ;;
+        r6tests) run pytest_r6 900 python -u -m pytest tests/test_gpu_mega.py tests/test_gpu_bench.py -x -v \
+                --timeout 300 --timeout-method thread || exit 1 ;;
         records) run pytest_records 600 python -u -m pytest tests/test_gpu.py -k "record or every_layout or golden or readme" \
                 -x -v --timeout 300 --timeout-method thread || exit 1 ;;
         *) echo "unknown step $step"; exit 2 ;;

@@ -631,8 +631,11 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
             return false;
         };
         if (!alloc(rec)) {
+            // the multi-line records without their walk line, then the one-line encodings
+            const uint32_t nowalk = (rec & kOccRecWalkBit) ? interleaved_record_bytes(v, true, false) : 0u;
             const uint32_t one = interleaved_record_bytes(v, false);
-            rec = one != rec && alloc(one) ? one : 0u;
+            if (nowalk != 0 && nowalk != rec && alloc(nowalk)) rec = nowalk;
+            else rec = one != rec && alloc(one) ? one : 0u;
         }
         if (rec != 0) {
             ix->rec_bytes = rec;
@@ -670,8 +673,8 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     ix->gkey_len = 0;
     if (S >= 2)
         for (uint64_t bins = S; bins <= kGroupBins && ix->gkey_len < 16; bins *= S) ++ix->gkey_len;
-    // on by default for launches of at least 2^20 patterns whose key spans at
-    // least 5 symbols (DNA: 6), and of at least 2^26 whose key is shorter (a
+    // on by default for launches of at least 3 x 2^20 patterns whose key spans
+    // at least 5 symbols (DNA: 6), and of at least 2^26 whose key is shorter (a
     // 20-residue alphabet keys on 3, no more than its k-mer seed: at 25.6 M
     // patterns per launch grouping lost, 3.29 vs 3.59 x 10^9, profiles/r5/
     // r5f_*; at 102.4 M it won, 3.68 vs 3.42-3.45, r5c4m_*).  Below ~1 M
@@ -679,8 +682,12 @@ static fmx_status finish_load(fmx_index *ix, uint32_t options) {
     // of 1,000 (C1) launch order runs 8.0 vs 4.2 x 10^9 grouped (r5p_*,
     // r5q_*), at 0.8 M patterns on 1 Gbp the two were equal and at 1.6 M
     // grouping gained 6 % (round 3); at 25.6 M patterns it gains 4 % on a
-    // 4 Mbp text and 50 % from 16 Mbp up (r5q_size_*, r5r_size_*).
-    ix->grouped_min = ix->gkey_len >= 5 ? (1ull << 20) : (1ull << 26);
+    // 4 Mbp text and 50 % from 16 Mbp up (r5q_size_*, r5r_size_*).  Round 6,
+    // C3's per-rank slabs on 1 Gbp (256 batches per launch, same box,
+    // profiles/r6/r6d_c3{g,o}_*): grouped vs launch order 2.97 vs 2.65 x 10^9
+    // at 5 M, 2.62 vs 2.61 at 2.5 M, 2.42 vs 2.54 at 1.6 M, 2.25 vs 2.48 at
+    // 1.25 M (C3's slab at 8 ranks) — the crossover is ~2.5 M, so 3 x 2^20.
+    ix->grouped_min = ix->gkey_len >= 5 ? (3ull << 20) : (1ull << 26);
     if (const char *e = getenv("FMX_GROUPED")) {
         if (e[0] == '0') ix->grouped_min = ~0ull;
         else if (e[0] == '1') ix->grouped_min = 1;

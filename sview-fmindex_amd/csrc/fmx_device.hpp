@@ -166,6 +166,7 @@ using V4 = uint32_t __attribute__((ext_vector_type(4)));
 constexpr int kRecPaired = 1;
 constexpr int kRecOneHot = 2;
 constexpr int kRecWalk = 4;
+static_assert(kRecWalk == (int)kOccRecWalkBit, "fmx_internal.hpp kOccRecWalkBit");
 
 // Whether record encoding rec (0, 64, 128, | kRecPaired, | kRecOneHot) can
 // hold a block of N planes of VB bits and at least one checkpoint of pos bytes.

@@ -117,6 +117,7 @@ constexpr uint8_t kNoDigit = 0xFF;
 #define FMX_OCC_WALK_DEFAULT 1
 #endif
 constexpr bool kOccWalkDefault = FMX_OCC_WALK_DEFAULT != 0;
+constexpr uint32_t kOccRecWalkBit = 4;  // = kRecWalk (fmx_device.hpp), for the host code that does not include it
 constexpr uint32_t kStatusSlots = 1024;   // status words per index (one per stream)
 constexpr uint64_t kKmerLdsMax = 4096;    // k-mer count tables up to this size are staged in LDS
 
@@ -522,7 +523,7 @@ hipError_t build_full_sa(fmx_index *ix, uint32_t stride, hipStream_t stream);
 hipError_t build_text(fmx_index *ix, hipStream_t stream);
 // Fill the context half of the row records (FMX_OPT_ROW_CONTEXT) from d_text.
 hipError_t build_row_context(fmx_index *ix, hipStream_t stream);
-uint32_t interleaved_record_bytes(const BlobView &bv, bool multi);
+uint32_t interleaved_record_bytes(const BlobView &bv, bool multi, bool walk_ok = true);
 
 // GPU builder (fmx_build.hip).
 fmx_status build_device(const uint8_t *d_text, uint64_t n, const uint8_t *table, uint32_t sigma,

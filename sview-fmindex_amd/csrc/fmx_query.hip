@@ -282,10 +282,10 @@ __global__ __launch_bounds__(256) void k_row_ctx(const QueryArgs a, uint64_t n, 
 // FMX_OCC_ONEHOT=0 / FMX_OCC_PAIRED=0 keep the next simpler record encoding
 // (A/B runs; results are identical); FMX_OCC_WALK=1 / 0: multi-line symbol
 // masks with / without a walk line (fmx_device.hpp kRecWalk; kOccWalkDefault)
-uint32_t interleaved_record_bytes(const BlobView &bv, bool multi) {
+uint32_t interleaved_record_bytes(const BlobView &bv, bool multi, bool walk_ok) {
     const char *ep = getenv("FMX_OCC_PAIRED"), *eh = getenv("FMX_OCC_ONEHOT"), *ew = getenv("FMX_OCC_WALK");
     const bool paired = !(ep && ep[0] == '0'), onehot = !(eh && eh[0] == '0');
-    const bool walk = ew ? ew[0] != '0' : kOccWalkDefault;
+    const bool walk = walk_ok && (ew ? ew[0] != '0' : kOccWalkDefault);
     return interleaved_rec_bytes(bv.L.pos_bytes, bv.L.planes, bv.L.vec_bits, bv.sigma, paired, onehot, multi, walk);
 }
 

@@ -273,9 +273,10 @@ def test_record_encodings(pkg, O, pb, planes, vb, monkeypatch):
 
 
 def test_record_fallback_when_hbm_is_short(pkg, O, monkeypatch):
-    """fmx_load falls back from multi-line symbol masks to the one-line
-    encodings, then to the blob layout, when the records do not fit in HBM
-    (FMX_OCC_MAX_MB stands in for a full device); answers are unchanged."""
+    """fmx_load falls back from multi-line symbol masks with a walk line to
+    those without, to the one-line encodings, then to the blob layout, when
+    the records do not fit in HBM (FMX_OCC_MAX_MB stands in for a full
+    device); answers are unchanged."""
     rng = np.random.default_rng(21)
     chars = rand_chr_list(rng, 21)
     table = table_from_symbols([bytes([c]) for c in chars])
@@ -283,7 +284,8 @@ def test_record_fallback_when_hbm_is_short(pkg, O, monkeypatch):
     blob = gpu_build(pkg, text, 21, 4, 5, 64, 3, 2, table)
     pats = [rand_pattern(rng, text, 1, 14) for _ in range(500)]
     blocks = len(text) // 64 + 1
-    for cap_mb, want in ((None, 384 | 2), ((blocks * 128 >> 20) + 1, 128), (0, 0)):
+    for cap_mb, want in ((None, 512 | 2 | 4), ((blocks * 384 >> 20) + 1, 384 | 2), ((blocks * 128 >> 20) + 1, 128),
+                         (0, 0)):
         if cap_mb is None:
             monkeypatch.delenv("FMX_OCC_MAX_MB", raising=False)
         else:

@@ -85,19 +85,25 @@ def test_rccl_world1_strong_job():
     assert r["hbm_per_rank"]["gather_slabs"] > 0
 
 
-def test_rccl_world1_weak_gather():
+@pytest.mark.parametrize("policy", ["all", "counts"])
+def test_rccl_world1_weak_gather(policy):
     """c2-shaped weak scaling under torchrun with one RCCL rank: each launch
-    group's counts and locations all-gathered by RCCL inside the timed step;
-    the assembled results hold this rank's part intact."""
+    group's counts and locations (`--gather all`) or counts alone (`--gather
+    counts`: the locations gathered once after the timed region) all-gathered
+    by RCCL inside the timed step; the assembled results hold this rank's part
+    intact, and the line states what each policy moves and needs."""
     p = run_bench(["--config", "c2", "--text-len", "20000000", "--patterns", "20000", "--group", "64", "--steps",
-                   "16", "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0"],
-                  env_extra={"FMX_BENCH_DIST": "1"}, torchrun=1)
+                   "16", "--batches", "16", "--no-cpu", "--min-seconds", "0.05", "--warmup", "0",
+                   "--gather", policy], env_extra={"FMX_BENCH_DIST": "1"}, torchrun=1)
     assert p.returncode == 0, p.stderr[-3000:]
     r = last_json(p.stdout)
     assert r["backend"] == "nccl" and r["rccl_world_size"] == 1 and r["scaling"] == "weak"
     g = r["gather"]
     assert g["inside_timed_step"] and g["collectives_per_launch"] == 1 and g["assembly_ok"]
     assert g["assembled_patterns"] == r["config"]["distinct_batches"] * 20000
+    assert g["policy"] == policy and g["bytes_gathered_per_pass"] == g["bytes_per_pass"][policy]
+    assert g["bytes_per_pass"]["counts"] < g["bytes_per_pass"]["all"]
+    assert g["required_gbs_per_gpu_at_n8"]["all"] > g["required_gbs_per_gpu_at_n8"]["counts"] > 0
 
 
 def test_rccl_oversubscription_refused():

@@ -157,7 +157,7 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
     monkeypatch.delenv("FMX_GROUPED", raising=False)
     monkeypatch.delenv("FMX_GROUPED_MIN", raising=False)
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
-    assert ix.info()["grouped_min"] == 1 << 20  # the default for a key of at least 5 symbols
+    assert ix.info()["grouped_min"] == 3 << 20  # the default for a key of at least 5 symbols
     ix.close()
     monkeypatch.setenv("FMX_GROUPED", "0")
     for mode in ("0", None):
@@ -180,7 +180,7 @@ def test_grouped_equals_launch_order(pkg, O, monkeypatch):
 
 
 def test_default_policy_by_alphabet(pkg, O, monkeypatch):
-    """Grouping is on by default for launches of at least 2^20 patterns where
+    """Grouping is on by default for launches of at least 3 x 2^20 patterns where
     the key spans at least 5 symbols (ACGT: 6), and from 2^26 for a
     20-residue alphabet (key of 3 symbols: no LF step beyond a k = 3 seed
     shared by the key alone — only a launch of ~100 M patterns shares
@@ -195,7 +195,7 @@ def test_default_policy_by_alphabet(pkg, O, monkeypatch):
         ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block5(pkg.Vector.U64), options=1)
         info = ix.info()
         assert info["group_key_len"] == want_len and info["group_key_base"] == len(chars)
-        assert info["grouped_min"] == (1 << 20 if on else 1 << 26)
+        assert info["grouped_min"] == (3 << 20 if on else 1 << 26)
         ix.close()
 
 

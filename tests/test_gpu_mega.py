@@ -4,7 +4,7 @@
     shape — four kernel-argument groups of 256, the launch's batch table
     (GroupTab) full at kMaxMega entries and staged in LDS by the kernels that
     see the whole launch — at the shipped defaults (no FMX_GROUPED forcing,
-    no refine pass, no device-side check): ~2^20 fixed-length patterns, so the
+    no refine pass, no device-side check): ~3.3 M fixed-length patterns, so the
     engine's own threshold groups it.  Every batch's counts, offsets, total
     and locations against the oracle (with_slice.rs:21-33, locate/mod.rs:14-37).
   * Fused launches (k_locate) on two streams at once, each launch over more
@@ -111,10 +111,10 @@ class Batches:
 
 
 def test_grouped_launch_1024_batches(pkg, O):
-    """One fmx_locate_group_async call of 1,024 batches (1,000-1,100 patterns
-    of 12-32 bp each, every third reversed; 1.07 M patterns) on a 4 Mbp ACGT
+    """One fmx_locate_group_async call of 1,024 batches (3,100-3,300 patterns
+    of 12-32 bp each, every third reversed; 3.28 M patterns) on a 4 Mbp ACGT
     index (u32/Block3<u64>, sr 2, k 3) at the shipped defaults: the launch is
-    grouped by the engine's own threshold (2^20 patterns), as ONE launch over
+    grouped by the engine's own threshold (3 x 2^20 patterns), as ONE launch over
     four kernel-argument groups; two rounds on the same random-byte
     workspaces, every batch against the oracle."""
     import torch
@@ -122,8 +122,8 @@ def test_grouped_launch_1024_batches(pkg, O):
     orc = O.OracleIndex(blob, O.layout(4, 3, 64, 0))
     ix = pkg.FmIndex.load(blob, pkg.u32, pkg.blocks.Block3(pkg.Vector.U64), options=1)
     info = ix.info()
-    assert info["group_key_len"] > 0 and info["grouped_min"] == 1 << 20, info
-    sizes = [int(x) for x in rng.integers(1000, 1101, size=1024)]
+    assert info["group_key_len"] > 0 and info["grouped_min"] == 3 << 20, info
+    sizes = [int(x) for x in rng.integers(3100, 3301, size=1024)]
     lengths = [12 + (j * 7) % 21 for j in range(1024)]
     assert sum(sizes) >= info["grouped_min"]
     bt = Batches(torch, ix, rng, text, sizes, lengths)

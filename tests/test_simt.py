@@ -491,7 +491,7 @@ def test_grouping_policy_simt(pkg, O, simt, monkeypatch):
         i = ix.info()
         ix.close()
         return i["group_key_len"], i["grouped_min"]
-    assert policy() == (6, 1 << 20)
+    assert policy() == (6, 3 << 20)
     monkeypatch.setenv("FMX_GROUPED_MIN", "5000")
     assert policy() == (6, 5000)
     monkeypatch.delenv("FMX_GROUPED_MIN")
