@@ -47,6 +47,9 @@
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   megatest test_gpu_mega.py (1,024-batch grouped launch, two-stream fused launches), test_gpu_fused.py,
 #            test_gpu_provenance.py
+#   sampledab  one-row results from the search's sampled row vs the walk (lib/ab/libfmx_walk.so): C2, C4, single
+#   c4knobs  C4: in-workgroup sort off, XCD deal off, vs default, alternating twice
+#   c4trace  one-stream kernel trace of C4
 #   thresh   C3 slabs of 5 M / 2.5 M / 1.6 M / 1.25 M patterns: grouped vs launch order
 #   tabab    C2 on this build vs lib/ab/libfmx_prev.so (the previous commit), alternating twice
 #   c4       bench.py --config c4 (with the CPU leg)
@@ -390,10 +393,36 @@ for step in "$@"; do
                 FMX_LIB=$PWD/sview-fmindex_amd/lib/ab/libfmx_prev.so run "tab_prev_$r" 400 $B || exit 1
             done ;;
         c4)  run bench_c4 400 python -u bench.py --config c4 || exit 1 ;;
+        paritycore) run pytest_core 1100 python -u -m pytest tests/test_gpu_full.py tests/test_gpu_mega.py \
+                tests/test_gpu_grouped.py tests/test_gpu_fused.py -x -v --timeout 300 --timeout-method thread || exit 1 ;;
         r6tests) run pytest_r6 900 python -u -m pytest tests/test_gpu_mega.py tests/test_gpu_bench.py -x -v \
                 --timeout 300 --timeout-method thread || exit 1 ;;
         records) run pytest_records 600 python -u -m pytest tests/test_gpu.py -k "record or every_layout or golden or readme" \
                 -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+        c4knobs)  # C4 grouped: the in-workgroup sort off (FMX_GROUPED_WSORT=0) and the XCD deal off (FMX_GROUPED_XCD=0)
+            # vs the default, alternating twice
+            B="python -u bench.py --config c4 --no-cpu --no-blob-layout --no-single-batch"
+            for r in 1 2; do
+                run "c4_def_$r" 400 $B || exit 1
+                FMX_GROUPED_WSORT=0 run "c4_nowsort_$r" 400 $B || exit 1
+                FMX_GROUPED_XCD=0 run "c4_noxcd_$r" 400 $B || exit 1
+            done ;;
+        c4trace)  # one-stream kernel trace of C4 (where a grouped launch's time goes)
+            run c4_trace 400 rocprofv3 --kernel-trace --stats -d "$OUT/c4trace" -o run --output-format csv -- \
+                python3 -u bench.py --config c4 --streams 1 --no-cpu --no-blob-layout --no-single-batch || exit 1
+            shrink "$OUT/c4trace" ;;
+        sampledab)  # one-row results located from the search's latest sampled row (this build) vs by the walk
+            # (sview-fmindex_amd/lib/ab/libfmx_walk.so, -DFMX_SAMPLED_ROW=0): C2, C4, single batch, alternating twice
+            B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
+            W=$PWD/sview-fmindex_amd/lib/ab/libfmx_walk.so
+            for r in 1 2; do
+                run "sr_c2_$r" 400 $B || exit 1
+                FMX_LIB=$W run "walk_c2_$r" 400 $B || exit 1
+                run "sr_c4_$r" 400 $B --config c4 || exit 1
+                FMX_LIB=$W run "walk_c4_$r" 400 $B --config c4 || exit 1
+                run "sr_single_$r" 300 python -u bench.py --single-batch-only || exit 1
+                FMX_LIB=$W run "walk_single_$r" 300 python -u bench.py --single-batch-only || exit 1
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

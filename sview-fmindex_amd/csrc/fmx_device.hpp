@@ -872,6 +872,22 @@ FMX_HD bool dlut_code(const QueryArgs &a, const Tables<P> &s, const PatView &pv,
     return !miss;
 }
 
+// The latest SAMPLED row of a search's single-row phase (round 6).  Once the
+// interval is one row r_j, every LF step maps it to the row of the suffix
+// one text position earlier, so the final row's location (what the locate
+// walk finds, locate/mod.rs:19-35) is SA[r_j] - (the steps taken since r_j).
+// If some r_j of that phase is a sampled row (r_j % sr == 0: its SA is
+// SAs[r_j / sr], suffix_array/mod.rs:100-105), the location is one sampled-SA
+// read — no walk step (E[walk] = sr - 1 steps of one record each, C2: ~1);
+// with sr = 2 and ~5 single-row steps at 1 Gbp, nearly every pattern has one.
+// valid = 0: none seen (walk the final row as before).
+template <typename P>
+struct SampledRow {
+    uint64_t slot;  // its SAs index
+    P off;          // LF steps since it
+    uint32_t valid;
+};
+
 // Kernel variants of the search (template parameter VAR):
 constexpr int kVarFaithful = 0;  // the blob's structures only (+ FMX_OCC_INTERLEAVED): no derived-index code
 constexpr int kVarDerived = 1;   // derived structures, short single-row tail compares
@@ -879,7 +895,7 @@ constexpr int kVarDerivedLong = 2;  // derived structures, vectorised long tail 
 
 template <typename P, int N, int VB, int REC, int VAR = kVarDerived>
 FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatView &pv, bool have, P w0, P w1,
-                              P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode);
+                              P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode, SampledRow<P> *smp);
 
 // k-mer seed + LF loop: FmIndex::get_pos_range (with_slice.rs:21-33).
 // Returns status bits (0 = ok).  The result is the interval [lo, hi) with
@@ -888,9 +904,9 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
 // (kHitOne / kHitMask, see scan_rows).  The count is always hi - lo.
 template <typename P, int N, int VB, int REC, int VAR = kVarDerived>
 FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv, P &lo, P &hi, P &rloc,
-                       uint64_t &mask, uint32_t &mode) {
+                       uint64_t &mask, uint32_t &mode, SampledRow<P> *smp = nullptr) {
     if constexpr (VAR == kVarFaithful) {
-        return search_seeded<P, N, VB, REC, VAR>(a, s, pv, false, P(0), P(0), lo, hi, rloc, mask, mode);
+        return search_seeded<P, N, VB, REC, VAR>(a, s, pv, false, P(0), P(0), lo, hi, rloc, mask, mode, smp);
     } else {
         uint64_t code;
         const bool have = dlut_code<P>(a, s, pv, code);
@@ -900,7 +916,7 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
             w0 = dl[0];
             w1 = dl[1];
         }
-        return search_seeded<P, N, VB, REC, VAR>(a, s, pv, have, w0, w1, lo, hi, rloc, mask, mode);
+        return search_seeded<P, N, VB, REC, VAR>(a, s, pv, have, w0, w1, lo, hi, rloc, mask, mode, smp);
     }
 }
 
@@ -909,8 +925,9 @@ FMX_HD uint32_t search(const QueryArgs &a, const Tables<P> &s, const PatView &pv
 // seed reach, or a single-row entry) was read.
 template <typename P, int N, int VB, int REC, int VAR>
 FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatView &pv, bool have, P w0, P w1,
-                              P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode) {
+                              P &lo, P &hi, P &rloc, uint64_t &mask, uint32_t &mode, SampledRow<P> *smp) {
     using O = Occ<P, N, VB, REC>;
+    if (smp) smp->valid = 0;
     constexpr bool LT = VAR == kVarDerivedLong, DER = VAR != kVarFaithful;
     const uint32_t sigma = a.sigma, k = a.k;
     const uint64_t m = pv.m;
@@ -949,6 +966,25 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
     bool scan = DER && a.ctx_len != 0;
     if (scan && a.strict)
         for (uint64_t j = 0; j < idx; ++j) scan &= pv.at(j) < sigma;
+    // the single-row phase's latest sampled row (SampledRow; only when the
+    // caller locates, and FMX_SAMPLED_ROW=0 builds keep the walk for A/B)
+    const bool track = FMX_SAMPLED_ROW && smp != nullptr && a.safull == nullptr;
+    uint64_t sslot = 0;
+    P soff = 0;
+    bool shave = false;
+    auto note = [&]() {
+        if (shave) soff += P(1);
+        if (hi - lo == P(1)) {
+            uint64_t rem;
+            const uint64_t sl = sr_div(a, (uint64_t)lo, rem);
+            if (rem == 0) {
+                sslot = sl;
+                soff = 0;
+                shave = true;
+            }
+        }
+    };
+    if (track) note();
     // LF loop: with_slice.rs:27-31, next_pos_range (locate/mod.rs:39-45)
     uint32_t c = idx > 0 ? pv.at(idx - 1) : 0;  // next symbol, fetched one step ahead
     while (lo < hi && idx > 0) {
@@ -982,6 +1018,12 @@ FMX_HD uint32_t search_seeded(const QueryArgs &a, const Tables<P> &s, const PatV
         c = idx > 0 ? pv.at(idx - 1) : 0;
         lo = pre + rlo;
         hi = pre + rhi;
+        if (track) note();
+    }
+    if (track && shave && hi - lo == P(1)) {
+        smp->slot = sslot;
+        smp->off = soff;
+        smp->valid = 1;
     }
     return 0;
 }
@@ -997,6 +1039,11 @@ FMX_HD T load_once(const T *p) {
     return *p;
 #endif
 }
+
+// The location of a one-row result: from the search's latest sampled row
+// (SampledRow: one sampled-SA read), else by the walk below.
+template <typename P, int N, int VB, int REC>
+FMX_HD P locate_one(const QueryArgs &a, const P *C, P row, const SampledRow<P> &smp);
 
 // Walk one suffix-array row to a sampled row or to the text start
 // (locate/mod.rs:19-35; suffix_array/mod.rs:100-105).
@@ -1018,6 +1065,12 @@ FMX_HD P walk_row(const QueryArgs &a, const P *C, P pos) {
         slot = sr_div(a, (uint64_t)pos, rem);
     }
     return load_once(reinterpret_cast<const P *>(a.sa) + slot) + off;
+}
+
+template <typename P, int N, int VB, int REC>
+FMX_HD P locate_one(const QueryArgs &a, const P *C, P row, const SampledRow<P> &smp) {
+    if (smp.valid) return load_once(reinterpret_cast<const P *>(a.sa) + smp.slot) - smp.off;
+    return walk_row<P, N, VB, REC>(a, C, row);
 }
 
 

@@ -117,7 +117,13 @@ constexpr uint8_t kNoDigit = 0xFF;
 #define FMX_OCC_WALK_DEFAULT 1
 #endif
 constexpr bool kOccWalkDefault = FMX_OCC_WALK_DEFAULT != 0;
-constexpr uint32_t kOccRecWalkBit = 4;  // = kRecWalk (fmx_device.hpp), for the host code that does not include it
+constexpr uint32_t kOccRecWalkBit = 4;
+// A one-row search result is located from the search's latest sampled row
+// when it has one (fmx_device.hpp SampledRow; build option for A/B: 0 walks
+// the final row as the reference does)
+#ifndef FMX_SAMPLED_ROW
+#define FMX_SAMPLED_ROW 1
+#endif  // = kRecWalk (fmx_device.hpp), for the host code that does not include it
 constexpr uint32_t kStatusSlots = 1024;   // status words per index (one per stream)
 constexpr uint64_t kKmerLdsMax = 4096;    // k-mer count tables up to this size are staged in LDS
 

@@ -347,15 +347,16 @@ __device__ __forceinline__ uint64_t search_lane(const QueryArgs &a, const Locate
     if (i < npat) {
         const PatView pv = pattern_view(s, s_pat, staged, bytes, beg, end, b0, b1, rev);
         P hi;
-        const uint32_t bad = search<P, N, VB, REC, VAR>(a, s, pv, lo, hi, rloc, mask, mode);
+        SampledRow<P> smp;
+        const uint32_t bad = search<P, N, VB, REC, VAR>(a, s, pv, lo, hi, rloc, mask, mode, &smp);
         if (bad) atomicOr(a.status, bad);
         cnt = (uint64_t)(hi - lo);
         if (B.out_cnt) reinterpret_cast<P *>(B.out_cnt)[i] = hi - lo;
         // one row (most patterns of a large text): its location now, while
-        // this lane's chain is live (locate/mod.rs:19-35); k_emit then only
-        // copies it
+        // this lane's chain is live (locate/mod.rs:19-35: from the search's
+        // latest sampled row, else by the walk); k_emit then only copies it
         if (mode == kHitRows && cnt == 1) {
-            rloc = walk_row<P, N, VB, REC>(a, s.C, lo);
+            rloc = locate_one<P, N, VB, REC>(a, s.C, lo, smp);
             mode = kHitOne;
         }
         if (mode == kHitOne) lo = 0;
@@ -1071,11 +1072,12 @@ __global__ __launch_bounds__(256, K == 2 ? 6 : 8) void k_search_grouped(const Qu
     uint32_t mode[K];
     if constexpr (K == 1) {
         if (!live[0]) return;
+        SampledRow<P> smp;
         const uint32_t bad = search<P, N, VB, REC, kVarFaithful>(a, s, pv[0], lo_r[0], hi_r[0], rloc[0], mask[0],
-                                                                  mode[0]);
+                                                                  mode[0], &smp);
         if (bad) atomicOr(a.status, bad);
         if (mode[0] == kHitRows && hi_r[0] - lo_r[0] == P(1)) {
-            rloc[0] = walk_row<P, N, VB, REC>(a, s.C, lo_r[0]);
+            rloc[0] = locate_one<P, N, VB, REC>(a, s.C, lo_r[0], smp);
             mode[0] = kHitOne;
         }
     } else {

@@ -182,13 +182,15 @@ int run(const orc_index &ox, uint32_t options, const uint8_t *bytes, const uint6
         // option bit 128: the long-pattern kernels' tail compare (LT)
         // the variant the engine launches (fmx_query.hip search_var)
         const bool derived = a.dlut || a.safull || a.text || a.ctx_len;
-        const uint32_t bad = !derived ? search<P, N, VB, REC, kVarFaithful>(a, t, pv, lo, hi, rloc, mask, mode)
-                             : long_tails ? search<P, N, VB, REC, kVarDerivedLong>(a, t, pv, lo, hi, rloc, mask, mode)
-                                          : search<P, N, VB, REC, kVarDerived>(a, t, pv, lo, hi, rloc, mask, mode);
+        SampledRow<P> smp;
+        const uint32_t bad =
+            !derived     ? search<P, N, VB, REC, kVarFaithful>(a, t, pv, lo, hi, rloc, mask, mode, &smp)
+            : long_tails ? search<P, N, VB, REC, kVarDerivedLong>(a, t, pv, lo, hi, rloc, mask, mode, &smp)
+                         : search<P, N, VB, REC, kVarDerived>(a, t, pv, lo, hi, rloc, mask, mode, &smp);
         if (bad) return bad == kStatusEmpty ? ORC_E_EMPTY_PATTERN : ORC_E_SYMBOL;
         const uint64_t cnt = (uint64_t)(hi - lo);
-        if (mode == kHitRows && cnt == 1) {  // k_search settles a single row by its walk
-            rloc = walk_row<P, N, VB, REC>(a, t.C, lo);
+        if (mode == kHitRows && cnt == 1) {  // k_search settles a single row (its sampled row, else its walk)
+            rloc = locate_one<P, N, VB, REC>(a, t.C, lo, smp);
             mode = kHitOne;
         }
         counts[i] = cnt;
