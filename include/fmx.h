@@ -234,7 +234,7 @@ fmx_status fmx_count_batch_async(fmx_index *ix, const uint8_t *d_bytes, const ui
                                  uint64_t n_patterns, uint32_t flags, void *d_counts, void *stream);
 
 /* Workspace for fmx_locate_batch_async, in bytes, for up to n_patterns patterns:
- * [256 B][32 KiB of key counters][50 KiB batch table of a grouped launch]
+ * [256 B][32 KiB of key counters][58 KiB batch table of a grouped launch]
  * [tile counts][tile offsets][one search record per pattern][to 16 B][one
  * 16-B sorted-order record per pattern].
  * The workspace must be 16-byte aligned (FMX_E_ARG otherwise: the grouped

@@ -480,6 +480,7 @@ struct GroupTab {
     uint32_t vfirst[kMaxMega];
     uint32_t first32[kMaxMega];
     uint16_t stride16[kMaxMega];
+    void *sorted[kMaxMega];  // = desc[j].sorted, compact for the place pass's staging (64 lines, not 256)
     GroupDesc desc[kMaxMega];
 };
 constexpr uint64_t kWsGroupTab = 256 + 4ull * kGroupCounterRoom;  // (16-B aligned)

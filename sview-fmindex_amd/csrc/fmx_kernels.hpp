@@ -643,9 +643,9 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     __shared__ U4 *s_sorted[PLACE ? kMaxMega : 1];
     const uint32_t t = threadIdx.x;
     if constexpr (PLACE)
-        for (uint32_t j = t; j < grp.gn; j += T) {
-            s_first[j] = (uint32_t)grp.gtab->first[j];
-            s_sorted[j] = reinterpret_cast<U4 *>(grp.gtab->desc[j].sorted);
+        for (uint32_t j = t; j < grp.gn; j += T) {  // (the compact copies: 96 lines per workgroup, not 320)
+            s_first[j] = grp.gtab->first32[j];
+            s_sorted[j] = reinterpret_cast<U4 *>(grp.gtab->sorted[j]);
         }
     if (t < 256) s_enc[t] = a.tab->enc[t];
     if (t < (uint32_t)kMaxSigma) s_dig[t] = a.tab->dig[t] == kNoDigit ? 0 : a.tab->dig[t];  // (absent: occurs nowhere)

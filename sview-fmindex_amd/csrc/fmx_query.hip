@@ -484,6 +484,7 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
             tab->vfirst[gn] = (vt + grp.tile_begin[j]) * 256u;
             tab->first32[gn] = (uint32_t)first;
             tab->stride16[gn] = (uint16_t)B.stride;
+            tab->sorted[gn] = reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + ((B.npat * rb + 15) & ~15ull);
             tab->desc[gn] = GroupDesc{reinterpret_cast<uint8_t *>(B.tiles + 2 * G),
                                       reinterpret_cast<uint8_t *>(B.tiles + 2 * G) + ((B.npat * rb + 15) & ~15ull),
                                       B.bytes, B.stride, B.rev};
@@ -519,6 +520,7 @@ static hipError_t launch_grouped(const fmx_index *ix, const QueryArgs &qa, Locat
     if ((e = put_bytes(d_tab->first, tab->first, 8ull * gn, stream)) != hipSuccess ||
         (e = put_bytes(d_tab->vfirst, tab->vfirst, offsetof(GroupTab, stride16) - offsetof(GroupTab, vfirst) +
                        2ull * gn, stream)) != hipSuccess ||
+        (e = put_bytes(d_tab->sorted, tab->sorted, sizeof(void *) * gn, stream)) != hipSuccess ||
         (e = put_bytes(d_tab->desc, tab->desc, sizeof(GroupDesc) * gn, stream)) != hipSuccess)
         return e;
     // the count pass needs each pattern's key alone: it reads and decodes only the key's bytes (the
