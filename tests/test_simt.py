@@ -226,7 +226,7 @@ def test_long_patterns_grouped_simt(pkg, O, simt, monkeypatch, m, pb, planes, vb
     pats += [b"N" * m, b"A" * m]
     g0 = grids(simt)
     check_simt(pkg, O, blob, pb, planes, vb, pats, 1, reversed_too=False)
-    assert grids(simt) - g0 == 11, ("not a grouped launch (load: relayout; locate: 3 x put (the batch table), key, "
+    assert grids(simt) - g0 == 12, ("not a grouped launch (load: relayout; locate: 4 x put (the batch table), key, "
                                     "scan, place, search, tiles, k_scan, emit)")
     check_simt(pkg, O, blob, pb, planes, vb, pats, 1)
 
