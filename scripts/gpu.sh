@@ -47,7 +47,7 @@
 #   megab    C2 at 256 / 512 / 1,024 batches per launch (one grouped launch over 2-4 kernel-argument groups), twice
 #   megatest test_gpu_mega.py (1,024-batch grouped launch, two-stream fused launches), test_gpu_fused.py,
 #            test_gpu_provenance.py
-#   nextab   this build vs lib/ab/libfmx_next.so (a candidate), C2 and C4, alternating twice
+#   prevab   this build vs lib/ab/libfmx_prev.so (the build before), C2 and C4, alternating twice
 #   sampledab  one-row results from the search's sampled row vs the walk (lib/ab/libfmx_walk.so): C2, C4, single
 #   c4knobs  C4: in-workgroup sort off, XCD deal off, vs default, alternating twice
 #   c4trace  one-stream kernel trace of C4
@@ -424,15 +424,15 @@ for step in "$@"; do
                 run "sr_single_$r" 300 python -u bench.py --single-batch-only || exit 1
                 FMX_LIB=$W run "walk_single_$r" 300 python -u bench.py --single-batch-only || exit 1
             done ;;
-        nextab)  # this tree's libfmx.so vs sview-fmindex_amd/lib/ab/libfmx_next.so (a candidate build), C2 and C4,
+        prevab)  # this tree's libfmx.so vs sview-fmindex_amd/lib/ab/libfmx_prev.so (the build before), C2 and C4,
             # alternating twice
             B="python -u bench.py --no-cpu --no-blob-layout --no-single-batch"
-            X=$PWD/sview-fmindex_amd/lib/ab/libfmx_next.so
+            X=$PWD/sview-fmindex_amd/lib/ab/libfmx_prev.so
             for r in 1 2; do
                 run "cur_c2_$r" 400 $B || exit 1
-                FMX_LIB=$X run "next_c2_$r" 400 $B || exit 1
+                FMX_LIB=$X run "prev_c2_$r" 400 $B || exit 1
                 run "cur_c4_$r" 400 $B --config c4 || exit 1
-                FMX_LIB=$X run "next_c4_$r" 400 $B --config c4 || exit 1
+                FMX_LIB=$X run "prev_c4_$r" 400 $B --config c4 || exit 1
             done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
