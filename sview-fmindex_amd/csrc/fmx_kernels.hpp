@@ -642,39 +642,6 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
     __shared__ uint32_t s_first[PLACE ? kMaxMega : 1];
     __shared__ U4 *s_sorted[PLACE ? kMaxMega : 1];
     const uint32_t t = threadIdx.x;
-    // G patterns' words in flight at once (all of a thread's when they are short)
-    constexpr uint32_t G = W <= 8 ? PPT : 1;
-    // (place, short patterns: one chunk, one group of loads) the chunk's
-    // pattern words are loaded before the tables are staged and the
-    // histogram cleared, so that their round trip overlaps the staging's
-    constexpr bool PRE = PLACE && G == PPT;
-    uint32_t xpre[PRE ? G : 1][W], lpre[PRE ? G : 1];
-    auto load_words = [&](const LocateBatch &Bl, uint64_t firstl, uint32_t p0, uint32_t (&x)[G][W],
-                          uint32_t (&lead)[G], uint64_t (&chk)[G]) {
-        const uint32_t m = Bl.stride, L = grp.gkey_len;
-        const bool rev = Bl.rev != 0;
-        // the bytes read: the whole pattern, or (RAW) its key's: the last kl
-        // input bytes, or the first kl of a reversed one
-        const uint32_t kl = L < m ? L : m, span = RAW ? kl : m;
-        const uint32_t skip = RAW && !rev ? m - kl : 0u;  // input bytes before the span
-#pragma unroll
-        for (uint32_t g = 0; g < G; ++g) {
-            const uint64_t i = firstl + (p0 + g) * T + t;
-            const uint64_t beg = i * m + skip, a0 = beg & ~3ull;
-            lead[g] = (uint32_t)(beg - a0);
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(Bl.bytes + a0);
-            const bool ok = i < Bl.npat;
-#pragma unroll
-            for (uint32_t q = 0; q < W; ++q) x[g][q] = ok && 4 * q < lead[g] + span ? src[q] : 0u;
-            chk[g] = ok && !PLACE ? Bl.offs[i + 1] : 0;
-        }
-    };
-    if constexpr (PRE) {
-        const uint32_t c = blockIdx.x, jb = group_chunk_batch(grp, c);
-        uint64_t chk_unused[G];
-        load_words(grp.b[jb], (uint64_t)(c - grp.chunk_begin[jb]) * kGroupChunkTiles * 256u, 0u, xpre, lpre,
-                   chk_unused);
-    }
     if constexpr (PLACE)
         for (uint32_t j = t; j < grp.gn; j += T) {  // (the compact copies: 96 lines per workgroup, not 320)
             s_first[j] = grp.gtab->first32[j];
@@ -721,22 +688,26 @@ __global__ __launch_bounds__(1024, W <= 8 ? 2 : 1) void k_group_key(const QueryA
         pn = n;
     }
     if (!PLACE && first == 0 && t == 0 && B.offs[0] != 0) atomicOr(a.status, kStatusStride);
+    // G patterns' words in flight at once (all of a thread's when they are short)
+    constexpr uint32_t G = W <= 8 ? PPT : 1;
 #pragma unroll
     for (uint32_t p0 = 0; p0 < PPT; p0 += G) {
     uint32_t x[G][W], lead[G];
     uint64_t chk[G];
+    // the bytes read: the whole pattern, or (RAW) its key's: the last kl
+    // input bytes, or the first kl of a reversed one
     const uint32_t kl = L < m ? L : m, span = RAW ? kl : m;
     const uint32_t skip = RAW && !rev ? m - kl : 0u;  // input bytes before the span
-    if constexpr (PRE) {
 #pragma unroll
-        for (uint32_t g = 0; g < G; ++g) {
-            lead[g] = lpre[g];
-            chk[g] = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint64_t i = first + (p0 + g) * T + t;
+        const uint64_t beg = i * m + skip, a0 = beg & ~3ull;
+        lead[g] = (uint32_t)(beg - a0);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(B.bytes + a0);
+        const bool ok = i < n;
 #pragma unroll
-            for (uint32_t q = 0; q < W; ++q) x[g][q] = xpre[g][q];
-        }
-    } else {
-        load_words(B, first, p0, x, lead, chk);
+        for (uint32_t q = 0; q < W; ++q) x[g][q] = ok && 4 * q < lead[g] + span ? src[q] : 0u;
+        chk[g] = ok && !PLACE ? B.offs[i + 1] : 0;
     }
 #pragma unroll
     for (uint32_t g = 0; g < G; ++g) {
@@ -1175,13 +1146,11 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
     const uint64_t g0 = (uint64_t)(blockIdx.x - grp.tile_begin[jb]) * E;
     const SearchRec<P> *__restrict__ recs = reinterpret_cast<const SearchRec<P> *>(B.tiles + 2 * G);
     P lo[E], rloc[E];
-    uint64_t mask[E], cnt[E], tbk[E];
+    uint64_t mask[E], cnt[E];
     uint32_t mode[E];
 #pragma unroll
     for (uint32_t k = 0; k < E; ++k) {
         const uint64_t i = (g0 + k) * 256u + threadIdx.x;
-        // the tile's offset (k_scan's) with the records, not after the barrier: one round trip, not two
-        tbk[k] = !fold && g0 + k < G ? B.tiles[G + g0 + k] : 0ull;
         lo[k] = rloc[k] = 0;
         mask[k] = cnt[k] = 0;
         mode[k] = kHitOne;
@@ -1226,7 +1195,7 @@ __global__ __launch_bounds__(256) void k_emit(const QueryArgs a, const LocateGro
             if (w < wv) before += s_scan[k][w];
             agg += s_scan[k][w];
         }
-        const uint64_t tb = fold ? base : tbk[k];
+        const uint64_t tb = fold ? base : B.tiles[G + g];
         const uint64_t my_off = tb + before + x[k] - cnt[k], i = g * 256u + threadIdx.x;
         if (fold && g == G - 1 && threadIdx.x == 0) {
             B.loc_off[npat] = tb + agg;
