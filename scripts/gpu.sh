@@ -356,6 +356,13 @@ for step in "$@"; do
             for t in 1000000 500000 250000 125000; do
                 run "c5_t$t" 500 python -u bench.py --config c5 --total-patterns $t $B || exit 1
             done ;;
+        c5trace)  # C5's per-rank slabs at N = 4 and 8 under the kernel trace (why 250 k runs slower than 125 k)
+            B="--no-cpu --no-blob-layout --no-single-batch"
+            for t in 250000 125000; do
+                run "c5trace_t$t" 400 rocprofv3 --kernel-trace --stats -d "$OUT/c5trace_$t" -o run --output-format csv -- \
+                    python3 -u bench.py --config c5 --total-patterns $t $B || exit 1
+                shrink "$OUT/c5trace_$t"
+            done ;;
         gloo2g)  # two gloo ranks on the one GPU, c2 weak, both gather policies
             FMX_BENCH_BACKEND=gloo run bench_gloo2_all 600 python -u bench.py --gpus 2 --no-cpu --gather all || exit 1
             FMX_BENCH_BACKEND=gloo run bench_gloo2_counts 600 python -u bench.py --gpus 2 --no-cpu --gather counts \
