@@ -97,3 +97,28 @@ def test_pack_patterns(pkg):
     data, off = pkg.pack_patterns([b"AC", b"", b"GGT"])
     assert data.tobytes() == b"ACGGT"
     assert off.tolist() == [0, 2, 2, 5]
+
+
+def test_workspace_bytes_host_sizing(pkg):
+    """fmx_workspace_bytes (ABI 8): the locate workspace a batch needs, from
+    the library's own arithmetic with no index loaded — what distributed.py's
+    per-rank HBM accounting uses.  Grows with n (a per-pattern record, a
+    16-B grouped record and two counters per tile), is wider for 8-B
+    positions, and rejects other position widths."""
+    ws = pkg.distributed.workspace_bytes
+    base4, base8 = ws(0, 4), ws(0, 8)
+    assert base4 > 0 and base8 >= base4
+    prev = base4
+    for n in (1, 255, 256, 257, 100_000, 102_400_000):
+        cur = ws(n, 4)
+        assert cur > prev and cur - base4 >= 16 * n
+        assert ws(n, 8) > cur
+        prev = cur
+    # linear in the tile count: 256 more patterns add one tile's worth exactly
+    assert ws(512, 4) - ws(256, 4) == ws(768, 4) - ws(512, 4)
+    for bad in (0, 2, 16):
+        with pytest.raises(ValueError):
+            ws(10, bad)
+    out = C.c_uint64()
+    assert pkg._native.lib().fmx_workspace_bytes(10, 4, None) != 0
+    assert pkg._native.lib().fmx_workspace_bytes(10, 4, C.byref(out)) == 0 and out.value == ws(10, 4)

@@ -127,6 +127,8 @@ def test_grouped_launch_1024_batches(pkg, O):
     lengths = [12 + (j * 7) % 21 for j in range(1024)]
     assert sum(sizes) >= info["grouped_min"]
     bt = Batches(torch, ix, rng, text, sizes, lengths)
+    # the index's workspace size = the host-only fmx_workspace_bytes (per-rank HBM accounting)
+    assert bt.ws_bytes == [pkg.distributed.workspace_bytes(n, 4) for n in sizes]
     bt.oracle(orc)
     q = bt.queue()
     torch.cuda.synchronize()
