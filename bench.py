@@ -166,6 +166,10 @@ def parse():
                          "counts and locations (north_star's single all-gather, default); counts: the count slabs "
                          "alone (the job's offsets on every rank), the locations gathered once after the timed "
                          "region")
+    ap.add_argument("--strong-groups", type=int, default=None,
+                    help="c3/c5: launch groups per rank, each of --group / this many batches (default with gathers — "
+                         "N > 1, or FMX_BENCH_DIST=1 — one per stream, so that one group's all-gather runs under "
+                         "the other's search; without: 1, the rank's batches in one launch)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment (weak configs): each launch group's patterns arranged so that workgroup "
@@ -645,7 +649,12 @@ def main():
     plan = job_starts = None
     if strong:
         # the global job (the same on every rank), dealt out by JobPlan
-        plan = D.JobPlan(total, world, B, GR)
+        # with gathers the job's results are gathered per launch group inside the step: one group per
+        # stream (each of GR / S batches), so that a group's gather overlaps the other group's search
+        SG = max(1, args.strong_groups if args.strong_groups is not None else (S if dist_on else 1))
+        if SG > 1:
+            GR = max(1, GR // SG)
+        plan = D.JobPlan(total, world, B, GR, min_groups=SG)
         jg_gen = torch.Generator(device=dev)
         jg_gen.manual_seed(args.seed * 1000 + 7)
         job_starts = torch.randint(0, n - m + 1, (total,), device=dev, dtype=torch.int64, generator=jg_gen)

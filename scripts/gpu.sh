@@ -356,6 +356,14 @@ for step in "$@"; do
             for t in 1000000 500000 250000 125000; do
                 run "c5_t$t" 500 python -u bench.py --config c5 --total-patterns $t $B || exit 1
             done ;;
+        shapes2)  # the per-rank shapes of gathered strong runs: two launch groups per rank (--strong-groups 2)
+            B="--no-cpu --no-blob-layout --no-single-batch --strong-groups 2"
+            for t in 10000000 5000000 2500000 1250000; do
+                run "c3sg2_t$t" 400 python -u bench.py --config c3 --total-patterns $t $B || exit 1
+            done
+            for t in 500000 250000 125000; do
+                run "c5sg2_t$t" 500 python -u bench.py --config c5 --total-patterns $t $B || exit 1
+            done ;;
         c5trace)  # C5's per-rank slabs at N = 4 and 8 under the kernel trace (why 250 k runs slower than 125 k)
             B="--no-cpu --no-blob-layout --no-single-batch"
             for t in 250000 125000; do

@@ -51,15 +51,20 @@ class JobPlan:
     on every rank.  So every rank issues nb / group launches of about the
     same size, and the ranks' pattern counts differ by at most one — the
     round-robin deal of fixed 100 k batches it replaces gave 8-GPU C5 a 2:1
-    imbalance (10 batches over 8 ranks)."""
+    imbalance (10 batches over 8 ranks).
 
-    def __init__(self, total: int, world: int, batch_target: int, group: int):
-        if total < 0 or world < 1 or batch_target < 1 or group < 1:
-            raise ValueError("JobPlan: total >= 0, world >= 1, batch_target >= 1, group >= 1")
+    min_groups: at least this many launch groups per rank (nb = group *
+    max(ceil(per / group), min_groups)) — bench.py's gathered strong runs
+    use one per stream, so that one group's all-gather runs under another
+    group's search instead of after the rank's only launch."""
+
+    def __init__(self, total: int, world: int, batch_target: int, group: int, min_groups: int = 1):
+        if total < 0 or world < 1 or batch_target < 1 or group < 1 or min_groups < 1:
+            raise ValueError("JobPlan: total >= 0, world >= 1, batch_target >= 1, group >= 1, min_groups >= 1")
         self.total, self.world, self.group = int(total), int(world), int(group)
         slab_max = -(-self.total // self.world)
         per = max(1, -(-slab_max // int(batch_target)))
-        self.nb = -(-per // self.group) * self.group
+        self.nb = max(-(-per // self.group), int(min_groups)) * self.group
         self.spans = [shard(self.total, self.world, r) for r in range(self.world)]
 
     @property

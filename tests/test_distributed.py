@@ -251,6 +251,27 @@ def test_job_plan_balanced(pkg, cfg, total, gr, world):
         assert plan.nb == 8 and sizes.max() == 15_625
 
 
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_job_plan_min_groups(pkg, world):
+    """bench.py's gathered strong runs: one launch group per stream (min_groups
+    = 2, each of GR / 2 batches) — C3 at 8 ranks keeps its 256 batches of
+    ~4.9 k as two groups of 128; C5 keeps 8 batches as two groups of 4; a
+    job smaller than min_groups batches still gets min_groups groups."""
+    D = pkg.distributed
+    for total, gr, nb_one in ((10_000_000, 256, 256), (1_000_000, 8, 8 if world > 1 else 16)):
+        one = D.JobPlan(total, world, 100_000, gr)
+        two = D.JobPlan(total, world, 100_000, gr // 2, min_groups=2)
+        assert one.nb == nb_one and one.groups == nb_one // gr
+        per = -(-(-(-total // world)) // 100_000)
+        assert two.nb == max(-(-per // (gr // 2)), 2) * (gr // 2) and two.groups == two.nb // (gr // 2) >= 2
+        assert int(two.sizes().sum()) == total and two.sizes().max() - two.sizes().min() <= 1
+        assert [b for r in range(world) for b in two.batches(r)][-1][1] == total
+    small = D.JobPlan(10, world, 100, 1, min_groups=3)
+    assert small.nb == 3 and small.groups == 3 and int(small.sizes().sum()) == 10
+    with pytest.raises(ValueError):
+        D.JobPlan(10, 1, 3, 2, min_groups=0)
+
+
 def test_job_gather_slots_one_rank(pkg):
     """World 1: the slab is the result; slots are exact, assembly is the
     concatenation of every batch in order."""
@@ -346,7 +367,8 @@ def test_hbm_per_rank_world8(pkg, cfg):
         .set_suffix_array_config(pkg.build_config.SuffixArrayConfig.Compressed(c["sr"])).blob_size()
     records = (c["text_len"] // c["vec"] + 1) * 128
     if c["total"]:
-        plan = D.JobPlan(c["total"], world, B, GR)
+        GR = max(1, GR // 2)  # bench.py's gathered strong runs: one launch group per stream (2)
+        plan = D.JobPlan(c["total"], world, B, GR, min_groups=2)
         sizes = [b - a for a, b in plan.batches(0)]
     else:
         sizes = [B] * (2 * GR)  # bench.py's default c2: two launch groups (one per stream)

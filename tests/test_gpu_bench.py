@@ -83,6 +83,9 @@ def test_rccl_world1_strong_job():
     assert rep["identical"] and rep["bytes"] > 0 and "broadcast" in rep["how"]
     assert r["parity"]["bit_exact_vs_cpu"] and r["parity"]["patterns"] == 800_000
     assert r["hbm_per_rank"]["gather_slabs"] > 0
+    # one launch group per stream (--strong-groups default), each of 256 / 2 batches
+    assert g["plan"]["launch_groups"] == r["config"]["streams"] == 2
+    assert r["config"]["batches_per_launch"] == 128 and g["plan"]["batches_per_rank"] == 256
 
 
 @pytest.mark.parametrize("policy", ["all", "counts"])
