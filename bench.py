@@ -167,9 +167,9 @@ def parse():
                          "alone (the job's offsets on every rank), the locations gathered once after the timed "
                          "region")
     ap.add_argument("--strong-groups", type=int, default=None,
-                    help="c3/c5: launch groups per rank, each of --group / this many batches (default with gathers — "
-                         "N > 1, or FMX_BENCH_DIST=1 — one per stream, so that one group's all-gather runs under "
-                         "the other's search; without: 1, the rank's batches in one launch)")
+                    help="c3/c5: launch groups per rank, each of --group / this many batches (default: one per stream, "
+                         "so that with N > 1 one group's all-gather runs under the other's search; 1: the rank's "
+                         "batches in one launch group)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment (weak configs): each launch group's patterns arranged so that workgroup "
@@ -649,9 +649,10 @@ def main():
     plan = job_starts = None
     if strong:
         # the global job (the same on every rank), dealt out by JobPlan
-        # with gathers the job's results are gathered per launch group inside the step: one group per
-        # stream (each of GR / S batches), so that a group's gather overlaps the other group's search
-        SG = max(1, args.strong_groups if args.strong_groups is not None else (S if dist_on else 1))
+        # one launch group per stream (each of GR / S batches): with gathers (N > 1) a group's gather
+        # overlaps the other group's search; without, the two launches overlap each other's tails
+        # (C3 10 M on one GPU 3.52 vs 3.39 x 10^9, C5 250 k 3.48 vs 2.54 x 10^8: profiles/r6/r6o_*)
+        SG = max(1, args.strong_groups if args.strong_groups is not None else S)
         if SG > 1:
             GR = max(1, GR // SG)
         plan = D.JobPlan(total, world, B, GR, min_groups=SG)
@@ -813,7 +814,8 @@ def main():
     # (the engine's policy: packable fixed-length launches from grouped_min patterns; longer patterns only
     # when FMX_GROUPED=1 / FMX_GROUPED_RAW=1 ask for it)
     packs = m * table.symbol_count().bit_length() <= 96 and os.environ.get("FMX_GROUPED_RAW") != "1"
-    grouped = bool(info.get("group_key_len")) and B * GR >= info["grouped_min"] and bool(fixed) and \
+    grouped = bool(info.get("group_key_len")) and max(grp["patterns"] for grp in w.groups) >= info["grouped_min"] \
+        and bool(fixed) and os.environ.get("FMX_GROUPED") != "0" and \
         (packs or os.environ.get("FMX_GROUPED") == "1" or os.environ.get("FMX_GROUPED_RAW") == "1")
     tr = traffic_of(args.traffic_json, key)
     roof = {
