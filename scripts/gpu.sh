@@ -364,6 +364,16 @@ for step in "$@"; do
             for t in 500000 250000 125000; do
                 run "c5sg2_t$t" 500 python -u bench.py --config c5 --total-patterns $t $B || exit 1
             done ;;
+        sgab)  # same box, alternating: one vs two launch groups per rank at the N = 1 and N = 8 shapes
+            B="--no-cpu --no-blob-layout --no-single-batch"
+            for i in 1 2; do
+                for sg in 1 2; do
+                    run "c3_sg${sg}_t10000000_$i" 400 python -u bench.py --config c3 $B --strong-groups $sg || exit 1
+                    run "c3_sg${sg}_t1250000_$i" 400 python -u bench.py --config c3 --total-patterns 1250000 $B \
+                        --strong-groups $sg || exit 1
+                    run "c5_sg${sg}_t1000000_$i" 500 python -u bench.py --config c5 $B --strong-groups $sg || exit 1
+                done
+            done ;;
         c5trace)  # C5's per-rank slabs at N = 4 and 8 under the kernel trace (why 250 k runs slower than 125 k)
             B="--no-cpu --no-blob-layout --no-single-batch"
             for t in 250000 125000; do
