@@ -167,9 +167,9 @@ def parse():
                          "alone (the job's offsets on every rank), the locations gathered once after the timed "
                          "region")
     ap.add_argument("--strong-groups", type=int, default=None,
-                    help="c3/c5: launch groups per rank, each of --group / this many batches (default: one per stream, "
-                         "so that with N > 1 one group's all-gather runs under the other's search; 1: the rank's "
-                         "batches in one launch group)")
+                    help="c3/c5: launch groups per rank, each of --group / this many batches (default with gathers — "
+                         "N > 1, or FMX_BENCH_DIST=1 — one per stream, so that one group's all-gather runs under "
+                         "the other's search; without: 1, the rank's batches in one launch group)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--xcd-partitioned", action="store_true",
                     help="experiment (weak configs): each launch group's patterns arranged so that workgroup "
@@ -649,10 +649,11 @@ def main():
     plan = job_starts = None
     if strong:
         # the global job (the same on every rank), dealt out by JobPlan
-        # one launch group per stream (each of GR / S batches): with gathers (N > 1) a group's gather
-        # overlaps the other group's search; without, the two launches overlap each other's tails
-        # (C3 10 M on one GPU 3.52 vs 3.39 x 10^9, C5 250 k 3.48 vs 2.54 x 10^8: profiles/r6/r6o_*)
-        SG = max(1, args.strong_groups if args.strong_groups is not None else S)
+        # with gathers (N > 1): one launch group per stream (each of GR / S batches), so that a group's
+        # gather runs under the other group's search; without, one group (same box, profiles/r6/r6q_*: C3
+        # 10 M 3.39 vs 3.28 x 10^9 and C5 1 M 3.50 vs 3.34 x 10^8 for one group, but C3's N = 8 slab
+        # 2.93 vs 2.61 x 10^9 for two)
+        SG = max(1, args.strong_groups if args.strong_groups is not None else (S if dist_on else 1))
         if SG > 1:
             GR = max(1, GR // SG)
         plan = D.JobPlan(total, world, B, GR, min_groups=SG)

@@ -43,7 +43,7 @@ def last_json(out):
 
 def test_c3_full_job_one_gpu():
     """BASELINE configs[2] (10 M x 20 bp over 1 Gbp) on one GPU: the job is
-    planned (256 batches of ~39 k, two grouped launches of 128: one per stream), every launch's
+    planned (256 batches of ~39 k, one grouped launch of 256), every launch's
     results are written into the exactly sized gather slabs, the job's flat
     (offsets, locations) is assembled on the device, and rank 0 compares all
     10 M counts and every location with the CPU oracle."""
@@ -56,7 +56,7 @@ def test_c3_full_job_one_gpu():
     assert r["parity"]["bit_exact_vs_cpu"], r["parity"]
     g = r["gather"]
     assert g["assembly_ok"] and g["needs_stable"] and g["assembled_patterns"] == 10_000_000
-    assert g["plan"]["batches_per_rank"] % 128 == 0 and g["plan"]["launch_groups"] == 2
+    assert g["plan"]["batches_per_rank"] % 128 == 0 and g["plan"]["launch_groups"] == 1
     assert r["config"]["launch_order"].startswith("grouped")
     assert r["self_location_check"] and r["n_gpus"] == 1 and r["ranks"] == 1
 
