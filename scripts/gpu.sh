@@ -313,6 +313,14 @@ for step in "$@"; do
             [ "${PMC_SKIP_TCC:-0}" = 1 ] && continue
             run pmc_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$OUT/pmc_tcc" -o run \
                 --output-format csv -- python3 -u bench.py $P || exit 1 ;;
+        pmcsq)  # one SQ pass (instruction mix and wait cycles per kernel), C2 and C4
+            for c in c2 c4; do
+                P="--config $c --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+                run "pmc_sq_$c" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU \
+                    SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace \
+                    -d "$OUT/pmc_sq_$c" -o run --output-format csv -- python3 -u bench.py $P || exit 1
+                shrink "$OUT/pmc_sq_$c"
+            done ;;
         configs)
             for c in c1 c3 c4 c5; do
                 run "bench_$c" 600 python -u bench.py --config $c || exit 1
