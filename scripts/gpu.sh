@@ -321,6 +321,13 @@ for step in "$@"; do
                     -d "$OUT/pmc_sq_$c" -o run --output-format csv -- python3 -u bench.py $P || exit 1
                 shrink "$OUT/pmc_sq_$c"
             done ;;
+        pmctlb)  # first-level address translation hits / misses per kernel, C2 and C4
+            for c in c2 c4; do
+                P="--config $c --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+                run "pmc_tlb_$c" 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_TRANSLATION_MISS_sum \
+                    --kernel-trace -d "$OUT/pmc_tlb_$c" -o run --output-format csv -- python3 -u bench.py $P || exit 1
+                shrink "$OUT/pmc_tlb_$c"
+            done ;;
         configs)
             for c in c1 c3 c4 c5; do
                 run "bench_$c" 600 python -u bench.py --config $c || exit 1
