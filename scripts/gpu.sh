@@ -328,6 +328,20 @@ for step in "$@"; do
                     --kernel-trace -d "$OUT/pmc_tlb_$c" -o run --output-format csv -- python3 -u bench.py $P || exit 1
                 shrink "$OUT/pmc_tlb_$c"
             done ;;
+        contigab)  # records in physically contiguous memory (FMX_OCC_CONTIG=1) vs hipMalloc's, same box, alternating;
+            # then the translation pass on C4 with them
+            B="--no-cpu --no-blob-layout --no-single-batch"
+            for i in 1 2; do
+                for c in c4 c2; do
+                    run "${c}_heap_$i" 400 python -u bench.py --config $c $B || exit 1
+                    FMX_OCC_CONTIG=1 run "${c}_contig_$i" 400 python -u bench.py --config $c $B || exit 1
+                done
+            done
+            P="--config c4 --streams 1 --no-cpu --no-blob-layout --no-single-batch --min-seconds 0.5"
+            FMX_OCC_CONTIG=1 run pmc_tlb_c4_contig 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_HIT_sum \
+                TCP_UTCL1_TRANSLATION_MISS_sum --kernel-trace -d "$OUT/pmc_tlb_c4_contig" -o run --output-format csv \
+                -- python3 -u bench.py $P || exit 1
+            shrink "$OUT/pmc_tlb_c4_contig" ;;
         configs)
             for c in c1 c3 c4 c5; do
                 run "bench_$c" 600 python -u bench.py --config $c || exit 1
