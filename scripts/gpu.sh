@@ -328,6 +328,12 @@ for step in "$@"; do
                     --kernel-trace -d "$OUT/pmc_tlb_$c" -o run --output-format csv -- python3 -u bench.py $P || exit 1
                 shrink "$OUT/pmc_tlb_$c"
             done ;;
+        walkab2)  # C4 walk-line records (default) vs without, now that most one-row results skip the walk
+            B="--config c4 --no-cpu --no-blob-layout --no-single-batch"
+            for i in 1 2 3; do
+                run "c4_walk_$i" 400 python -u bench.py $B || exit 1
+                FMX_OCC_WALK=0 run "c4_nowalk_$i" 400 python -u bench.py $B || exit 1
+            done ;;
         contigab)  # records in physically contiguous memory (FMX_OCC_CONTIG=1) vs hipMalloc's, same box, alternating;
             # then the translation pass on C4 with them
             B="--no-cpu --no-blob-layout --no-single-batch"
