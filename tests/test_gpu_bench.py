@@ -132,6 +132,8 @@ def test_gloo_two_ranks_one_gpu_strong():
     assert g["inside_timed_step"] and g["collectives_per_launch"] == 1 and g["assembly_ok"]
     assert g["gathered_over_result"] <= 1.25
     assert g["plan"]["patterns_per_rank"] == [400_000, 400_000]
+    # with gathers: one launch group per stream and rank (each group's gather overlaps the other's search)
+    assert g["plan"]["launch_groups"] == r["config"]["streams"] == 2 and r["config"]["batches_per_launch"] == 128
     assert r["parity"]["bit_exact_vs_cpu"] and r["parity"]["patterns"] == 800_000
     rep = r["blob_replication"]  # rank 0's blob broadcast to rank 1, checksums equal
     assert rep["identical"] and rep["bytes"] > 0
